@@ -1,0 +1,28 @@
+# Build the MI355X (gfx950) aggregation library and the CPU oracle helpers.
+#   make            -> byzantine_aircomp_amd/libgmagg.so
+#   make clean
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+CSRC     := byzantine_aircomp_amd/csrc
+BUILD    := build/obj
+LIB      := byzantine_aircomp_amd/libgmagg.so
+HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-result \
+            -I include -munsafe-fp-atomics
+SRCS     := $(CSRC)/weiszfeld.hip $(CSRC)/oma.hip $(CSRC)/api.hip
+OBJS     := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(SRCS))
+HDRS     := $(wildcard $(CSRC)/*.h) include/gmagg.h
+
+all: $(LIB)
+
+$(BUILD)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -L/opt/rocm/lib -lrccl \
+	    -Wl,-rpath,/opt/rocm/lib
+
+clean:
+	rm -rf $(BUILD) $(LIB)
+
+.PHONY: all clean

@@ -1,0 +1,187 @@
+"""Benchmark: geometric-median aggregations/sec at K=1000, d=11M (BASELINE.json).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (the driver's N>1 form)
+
+One step = one full `gm2` aggregation (BASELINE config C3): the initial
+distance pass plus Weiszfeld iterations until the reference's tol test
+(||g_t - g_{t+1}|| <= 1e-5) fires, on a synthetic K=1000 x d=11M fp32 client
+matrix already resident in HBM (honest rows ~ N(0, 0.05^2), the last 20% ~
+N(0.25, 0.5^2), guess ~ N(0, 0.01^2); generated on the device by Philox).
+
+N > 1: d is sharded over the ranks (256-aligned contiguous column shards),
+each Weiszfeld iteration all-reduces a (K+2)-vector of fp64 partials over RCCL
+(xGMI), every rank takes the same stop decision; total work is fixed, so
+scaling is "strong".  value = aggregations/s of the whole job.
+
+Rank 0 prints ONE JSON line.  `roofline` prices the dominant kernel (the fused
+streaming pass: 4*K*d_local algorithmic bytes per launch) with HIP events the
+library records around every launch on its stream; `cpu_baseline` times the
+CPU oracle (an op-for-op PyTorch-CPU restatement of the reference's gm2) on a
+bounded sample on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+WORKLOADS = {
+    # name: (K, d, byzantine rows)
+    "c3": (1000, 11_000_000, 200),
+    "c3-small": (1000, 1_000_000, 200),
+    "c4-shard": (256, 15_625_000, 51),     # one GPU's shard of K=256 x d=125M
+    "c5-problem": (50, 100_000, 10),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    p.add_argument("--algo", default="auto", choices=["auto", "stream", "twopass"])
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    p.add_argument("--cpu-d", type=int, default=2_000_000, help="CPU sample width")
+    return p.parse_args()
+
+
+def shard_range(d, n, r, align=256):
+    per = -(-d // n)
+    per = -(-per // align) * align
+    lo = min(d, r * per)
+    return lo, min(d, lo + per)
+
+
+def cpu_baseline(X, g0, iters, d_full):
+    """Time the oracle gm2 (PyTorch CPU, op-for-op the reference) on a sample."""
+    from oracle import aggregators as orc
+    threads = torch.get_num_threads()
+    Xc, gc = X.cpu(), g0.cpu()
+    t0 = time.perf_counter()
+    _, tr = orc.gm2(Xc, {"maxiter": iters, "tol": -1.0, "guess": gc})
+    dt = time.perf_counter() - t0
+    K, d = Xc.shape
+    per_agg_full = dt * (d_full / d)
+    return {"value": 1.0 / per_agg_full, "unit": "aggregations/s", "cores": threads,
+            "kind": "port",
+            "sample": (f"oracle gm2 (torch CPU, {threads} threads) on the first {d} columns "
+                       f"of the same K={K} matrix, {iters} Weiszfeld iterations (the GPU's "
+                       f"converged count; tol disabled), {dt:.2f} s, extrapolated linearly "
+                       f"in d to {d_full}")}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd import _lib
+
+    K, d_total, B = WORKLOADS[args.workload]
+    lo, hi = shard_range(d_total, world, rank)
+    d = hi - lo
+    ctx = bz.context(dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        ctx.set_shard(d_total, lo)
+        uid = [None]
+        if rank == 0:
+            import ctypes as C
+            buf = C.create_string_buffer(128)
+            _lib.check(ctx.lib.gm_rccl_get_unique_id(buf), "gm_rccl_get_unique_id")
+            uid[0] = buf.raw
+        dist.broadcast_object_list(uid, src=0)
+        ctx.init_rccl(uid[0], world, rank)
+
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    X = torch.empty(K, d, dtype=torch.float32, device=dev)
+    _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, X.data_ptr(), K, d, d, B, 0.0, 0.05, 0.25,
+                                           0.5, 20211, stream), "fill")
+    g0 = torch.empty(d, dtype=torch.float32, device=dev)
+    _lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), d, 0.0, 0.01, 20212, stream),
+               "fill")
+    opts = {"maxiter": 1000, "tol": 1e-5, "guess": g0, "algo": args.algo}
+
+    def step():
+        return bz.gm2(X, opts)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    ctx.pass_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    t1 = time.perf_counter()
+    pass_ms, launches = ctx.pass_timing(False)
+    res = bz.aggregators.last_result
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        per_launch_bytes = 4.0 * K * d
+        avg_pass_s = (pass_ms / 1e3) / max(launches, 1)
+        achieved = per_launch_bytes / avg_pass_s / 1e9
+        line = {
+            "metric": "GM aggregations/sec at K=1000,d=11M; % HBM roofline; 1/2/4/8 GPUs",
+            "value": args.steps / elapsed,
+            "unit": "aggregations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (Philox on device: honest N(0,0.05^2), last 20% N(0.25,0.5^2), "
+                    "guess N(0,0.01^2))",
+            "config": {"workload": f"{args.workload}: gm2 K={K} x d={d_total} fp32, B={B} "
+                                   f"Byzantine, tol 1e-5, maxiter 1000",
+                       "K": K, "d": d_total, "byzantine": B, "iters": res.iters,
+                       "algo": res.algo, "parallelism": f"d-shard x{world}" if world > 1 else "none",
+                       "passes_per_aggregation": res.iters + 1},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "weiszfeld_pass (STEP)", "launches_timed": launches,
+                         "avg_launch_us": avg_pass_s * 1e6,
+                         "algorithmic_bytes_per_launch": per_launch_bytes},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu:
+            dc = min(args.cpu_d, d)
+            line["cpu_baseline"] = cpu_baseline(X[:, :dc].contiguous(), g0[:dc], res.iters, d_total)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+    del out
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,13 @@
+"""MI355X-native geometric-median aggregation (Byzantine_AirComp hot path).
+
+Drop-in replacements for the reference's aggregators, backed by hand-written
+HIP kernels for gfx950 behind a C ABI (include/gmagg.h, libgmagg.so):
+
+    from byzantine_aircomp_amd import gm2, gm, OMA
+
+See DESIGN.md for the kernels and INTEGRATION.md for swapping them into the
+reference's training loop.
+"""
+from .aggregators import GMResult, OMA, context, gm, gm2  # noqa: F401
+
+__version__ = "0.1.0"

@@ -1,0 +1,272 @@
+"""Drop-in aggregators backed by libgmagg.so (HIP kernels for gfx950).
+
+The reference resolves its aggregator with ``eval(args.agg)``
+(MNIST_Air_weight.py:580) and calls it once per step as
+``weight_vector = aggregate(weight_f, options)`` (M:353).  This module provides
+functions with the same names, signatures, option keys, defaults and return
+semantics, so the reference's training loop can import them in place of its
+own:
+
+  ``gm2(wList, options)``  ideal Weiszfeld geometric median      (M:162-184)
+  ``gm(wList, options)``   AirComp Weiszfeld, OMA2 every step    (M:131-160, M:396-414)
+  ``OMA(message, noise_var)``  in-place per-client pre-noise     (M:385-394)
+
+Semantics kept from the reference:
+  * option keys ``maxiter`` (default 200), ``tol`` (1e-5), ``guess`` (default
+    the row mean), plus ``noise_var`` (None) and ``P_max`` (1) for ``gm``;
+    ``eta`` / ``honestSize`` are ignored, as in the reference;
+  * ``maxiter == 0`` returns the ``guess`` object itself;
+  * ``wList`` and ``guess`` are not modified (``OMA`` modifies ``message``);
+  * the result lives on ``wList.device``: a CPU input is staged to the GPU and
+    the aggregate copied back (the reference's hot path runs on CPU tensors);
+  * the tol test is on the fp32 movement, returning the NEW iterate.
+
+Extensions (ignored by the reference's loop): options ``noise_source``
+(``"device"``: on-device Philox, the default; ``"host"``: the reference's own
+``torch.normal`` draws on the CPU generator, in its order, for exact
+comparison), ``seed`` (Philox key; drawn from the torch CPU generator when
+absent) and ``algo`` (``"auto"``, ``"stream"``, ``"twopass"``).  The trace of
+the last call (iterations, last movement) is in ``last_result``.
+
+There is no CPU path: without a GPU or without libgmagg.so these raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+__all__ = ["gm2", "gm", "OMA", "GMResult", "last_result", "Context", "context"]
+
+
+@dataclass
+class GMResult:
+    iters: int
+    last_movement: float
+    converged: bool
+    algo: str
+
+
+last_result: GMResult | None = None
+_ALGOS = {"auto": _lib.GM_ALGO_AUTO, "stream": _lib.GM_ALGO_STREAM,
+          "twopass": _lib.GM_ALGO_TWOPASS, "gram": _lib.GM_ALGO_GRAM}
+_ALGO_NAMES = {v: k for k, v in _ALGOS.items()}
+
+
+class Context:
+    """One libgmagg context (device workspace, optional d-shard / RCCL comm)."""
+
+    def __init__(self, device: int):
+        self.lib = _lib.load()
+        self.device = device
+        h = C.c_void_p()
+        _lib.check(self.lib.gm_ctx_create(device, C.byref(h)), "gm_ctx_create")
+        self.handle = h
+        self._keep = []   # ctypes callbacks that must outlive the context
+
+    def set_shard(self, d_total: int, d_offset: int):
+        _lib.check(self.lib.gm_ctx_set_shard(self.handle, d_total, d_offset), "gm_ctx_set_shard")
+
+    def set_allreduce(self, fn):
+        """fn(dev_ptr:int, count:int, stream:int) -> None; sums doubles in place."""
+        def tramp(user, buf, count, stream):
+            try:
+                fn(buf, count, stream)
+                return 0
+            except Exception:  # noqa: BLE001 - reported through the status code
+                return 1
+        cb = _lib.ALLREDUCE_CB(tramp)
+        self._keep.append(cb)
+        _lib.check(self.lib.gm_ctx_set_allreduce(self.handle, cb, None), "gm_ctx_set_allreduce")
+
+    def init_rccl(self, unique_id: bytes, nranks: int, rank: int):
+        buf = C.create_string_buffer(bytes(unique_id), 128)
+        _lib.check(self.lib.gm_ctx_init_rccl(self.handle, buf, nranks, rank), "gm_ctx_init_rccl")
+
+    def pass_timing(self, enable: bool):
+        """Return (total_ms, launches) of the fused pass since the last call."""
+        ms, n = C.c_double(), C.c_int64()
+        _lib.check(self.lib.gm_ctx_pass_timing(self.handle, int(enable), C.byref(ms),
+                                               C.byref(n)), "gm_ctx_pass_timing")
+        return ms.value, n.value
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                self.lib.gm_ctx_destroy(self.handle)
+        except Exception:  # noqa: BLE001 - interpreter teardown
+            pass
+
+
+_contexts: dict[int, Context] = {}
+
+
+def context(device: torch.device | int | None = None) -> Context:
+    if not torch.cuda.is_available():
+        raise RuntimeError("byzantine_aircomp_amd needs a ROCm GPU (torch.cuda.is_available() "
+                           "is False); there is no CPU fallback")
+    if device is None:
+        idx = torch.cuda.current_device()
+    elif isinstance(device, int):
+        idx = device
+    else:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+    ctx = _contexts.get(idx)
+    if ctx is None:
+        ctx = _contexts[idx] = Context(idx)
+    return ctx
+
+
+def _stream_ptr(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _stage(t: torch.Tensor) -> torch.Tensor:
+    """The GPU tensor the kernels read (a copy if `t` lives on the CPU)."""
+    if t.dtype != torch.float32:
+        raise TypeError(f"aggregation kernels are fp32 (got {t.dtype})")
+    if t.device.type == "cuda":
+        return t
+    return t.to(torch.device("cuda", torch.cuda.current_device()))
+
+
+def _rows(X: torch.Tensor):
+    """(tensor, ldx) with unit column stride, rows >= d apart."""
+    if X.dim() != 2:
+        raise ValueError(f"wList must be [K, d] (got {tuple(X.shape)})")
+    if X.stride(1) != 1 or X.stride(0) < X.shape[1] or X.shape[0] == 0:
+        X = X.contiguous()
+    return X, max(X.stride(0), X.shape[1])
+
+
+def _noise_source(options) -> int:
+    src = options.get("noise_source", os.environ.get("BYZ_AIRCOMP_NOISE", "device"))
+    if src == "device":
+        return _lib.GM_NOISE_PHILOX
+    if src == "host":
+        return _lib.GM_NOISE_HOST
+    raise ValueError(f"noise_source must be 'device' or 'host' (got {src!r})")
+
+
+def _seed(options) -> int:
+    if options.get("seed") is not None:
+        return int(options["seed"]) & (2 ** 64 - 1)
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+def _host_draws(K: int, d: int, noise_var):
+    """The reference's OMA2 draws, in order, on the global CPU generator (M:401-411)."""
+    def cb(user, it, hr, hi, n):
+        try:
+            a = torch.normal(torch.zeros(K), 1 / math.sqrt(2))
+            b = torch.normal(torch.zeros(K), 1 / math.sqrt(2))
+            C.memmove(hr, a.data_ptr(), 4 * K)
+            C.memmove(hi, b.data_ptr(), 4 * K)
+            if noise_var is not None:
+                z = torch.normal(torch.zeros(d + 1), math.sqrt(noise_var / 2))
+                C.memmove(n, z.data_ptr(), 4 * (d + 1))
+            return 0
+        except Exception:  # noqa: BLE001
+            return 1
+    return _lib.NOISE_CB(cb)
+
+
+def _weiszfeld(wList: torch.Tensor, options: dict, aircomp: bool):
+    global last_result
+    opts = {"maxiter": 200, "tol": 1e-5}
+    if aircomp:
+        opts.update({"noise_var": None, "P_max": 1})
+    opts.update(options or {})
+    guess = opts.get("guess")
+    if guess is None:
+        guess = wList.mean(dim=0)
+    maxiter = int(opts["maxiter"])
+    if maxiter <= 0:                        # M:145 / M:173 loop body never runs
+        last_result = GMResult(0, float("nan"), False, "none")
+        return guess
+    X = _stage(wList)
+    X, ldx = _rows(X)
+    K, d = X.shape
+    g0 = guess.detach().to(device=X.device, dtype=torch.float32).contiguous()
+    if g0.numel() != d:
+        raise ValueError(f"guess has {g0.numel()} elements, wList rows have {d}")
+    out = torch.empty(d, dtype=torch.float32, device=X.device)
+    if d == 0:
+        last_result = GMResult(1, 0.0, True, "none")
+        return out.to(wList.device)
+
+    o = _lib.GmOpts()
+    o.maxiter = maxiter
+    o.tol = float(opts["tol"])
+    o.eps = 1e-4
+    o.mode = _lib.GM_MODE_AIRCOMP if aircomp else _lib.GM_MODE_IDEAL
+    o.algo = _ALGOS[opts.get("algo", "auto")]
+    o.check_every = int(opts.get("check_every", 0))
+    cb = None
+    if aircomp:
+        var = opts["noise_var"]
+        o.has_noise = int(var is not None)
+        o.noise_var = float(var) if var is not None else 0.0
+        o.P_max = float(opts["P_max"])
+        o.noise_source = _noise_source(opts)
+        if o.noise_source == _lib.GM_NOISE_HOST:
+            cb = _host_draws(K, d, var)
+            o.noise_cb = cb
+        else:
+            o.seed = _seed(opts)
+    ctx = context(X.device)
+    res = _lib.GmResult()
+    with torch.cuda.device(X.device):
+        _lib.check(ctx.lib.gm_weiszfeld_f32(ctx.handle, X.data_ptr(), K, d, ldx, g0.data_ptr(),
+                                            out.data_ptr(), C.byref(o), C.byref(res),
+                                            _stream_ptr(X.device)), "gm_weiszfeld_f32")
+    last_result = GMResult(res.iters, res.last_movement, bool(res.converged),
+                           _ALGO_NAMES.get(res.algo_used, "?"))
+    return out if wList.device == out.device else out.to(wList.device)
+
+
+def gm2(wList, options={}):  # noqa: B006 - the reference's signature (M:162)
+    """Ideal Weiszfeld geometric median (MNIST_Air_weight.py:162-184)."""
+    return _weiszfeld(wList, options, aircomp=False)
+
+
+def gm(wList, options={}):  # noqa: B006 - the reference's signature (M:131)
+    """AirComp Weiszfeld geometric median (MNIST_Air_weight.py:131-160)."""
+    return _weiszfeld(wList, options, aircomp=True)
+
+
+def OMA(message, noise_var=0.01, noise_source=None, seed=None):  # noqa: N802 - reference name
+    """In-place per-client equalised AWGN (MNIST_Air_weight.py:385-394)."""
+    if message.dtype != torch.float32:
+        raise TypeError(f"OMA kernel is fp32 (got {message.dtype})")
+    X = _stage(message)
+    Xc = X if (X.stride(1) == 1 and X.stride(0) >= X.shape[1]) else X.contiguous()
+    K, d = Xc.shape
+    ldx = max(Xc.stride(0), d)
+    ctx = context(Xc.device)
+    src = _noise_source({} if noise_source is None else {"noise_source": noise_source})
+    stream = _stream_ptr(Xc.device)
+    with torch.cuda.device(Xc.device):
+        if src == _lib.GM_NOISE_HOST:
+            sd = math.sqrt(noise_var)
+            hr = torch.normal(torch.zeros(K, 1), 1 / math.sqrt(2))     # M:389-392 order
+            hi = torch.normal(torch.zeros(K, 1), 1 / math.sqrt(2))
+            nr = torch.normal(torch.zeros(K, d), sd)
+            ni = torch.normal(torch.zeros(K, d), sd)
+            dev = [t.to(Xc.device) for t in (hr, hi, nr, ni)]
+            _lib.check(ctx.lib.gm_oma_apply_f32(ctx.handle, Xc.data_ptr(), K, d, ldx,
+                                                *[t.data_ptr() for t in dev], stream),
+                       "gm_oma_apply_f32")
+        else:
+            s = _seed({"seed": seed})
+            _lib.check(ctx.lib.gm_oma_philox_f32(ctx.handle, Xc.data_ptr(), K, d, ldx,
+                                                 float(noise_var), s, stream),
+                       "gm_oma_philox_f32")
+    if Xc is not message:
+        message.copy_(Xc)
+    return message

@@ -1,0 +1,509 @@
+// C ABI of libgmagg.so (include/gmagg.h): contexts, workspace, the Weiszfeld
+// host loop, OMA and the synthetic fills.
+//
+// The host loop mirrors the reference's control flow (MNIST_Air_weight.py:145-160
+// for gm, 173-184 for gm2) but keeps every decision on the device: the
+// K-space kernel sets a `done` word that makes later launches no-ops, and the
+// host only polls it every `check_every` iterations.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gmagg.h"
+#include "gmagg_internal.h"
+
+using namespace gmk;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                    \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(GM_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),    \
+                  __FILE__, __LINE__);                                                  \
+  } while (0)
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace
+
+struct gm_ctx {
+  int device = 0;
+  int num_cu = 256;
+  int64_t d_total = -1;   // -1: unsharded
+  int64_t d_offset = 0;
+  gm_allreduce_cb ar_fn = nullptr;
+  void* ar_user = nullptr;
+  ncclComm_t comm = nullptr;
+  char* ws = nullptr;
+  size_t ws_bytes = 0;
+  char* host = nullptr;   // pinned: KState mirror + host-noise staging
+  size_t host_bytes = 0;
+  bool timing = false;
+  std::vector<hipEvent_t> ev_free;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used;
+};
+
+namespace {
+
+struct Workspace {
+  KState* st;
+  double* sums;
+  double* r;
+  float* coef;
+  double* slab;
+  float* g[2];
+  float* h_re;   // host-noise device copies
+  float* h_im;
+  float* hnoise; // d local + 1
+};
+
+int ensure_ws(gm_ctx* c, int64_t K, int64_t d, int nb, Workspace* w) {
+  const int64_t S = 2 * K + 2;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
+  const size_t o_st = take(sizeof(KState));
+  const size_t o_sums = take(sizeof(double) * S);
+  const size_t o_r = take(sizeof(double) * K);
+  const size_t o_coef = take(sizeof(float) * K);
+  const size_t o_slab = take(sizeof(double) * S * (size_t)nb);
+  const size_t o_g0 = take(sizeof(float) * d);
+  const size_t o_g1 = take(sizeof(float) * d);
+  const size_t o_hr = take(sizeof(float) * K);
+  const size_t o_hi = take(sizeof(float) * K);
+  const size_t o_hn = take(sizeof(float) * (d + 1));
+  if (off > c->ws_bytes) {
+    if (c->ws) HIPCHK(hipFree(c->ws));
+    c->ws = nullptr;
+    c->ws_bytes = 0;
+    HIPCHK(hipMalloc(&c->ws, off));
+    c->ws_bytes = off;
+  }
+  char* b = c->ws;
+  w->st = reinterpret_cast<KState*>(b + o_st);
+  w->sums = reinterpret_cast<double*>(b + o_sums);
+  w->r = reinterpret_cast<double*>(b + o_r);
+  w->coef = reinterpret_cast<float*>(b + o_coef);
+  w->slab = reinterpret_cast<double*>(b + o_slab);
+  w->g[0] = reinterpret_cast<float*>(b + o_g0);
+  w->g[1] = reinterpret_cast<float*>(b + o_g1);
+  w->h_re = reinterpret_cast<float*>(b + o_hr);
+  w->h_im = reinterpret_cast<float*>(b + o_hi);
+  w->hnoise = reinterpret_cast<float*>(b + o_hn);
+  return GM_OK;
+}
+
+int ensure_host(gm_ctx* c, size_t bytes) {
+  if (bytes <= c->host_bytes) return GM_OK;
+  if (c->host) HIPCHK(hipHostFree(c->host));
+  c->host = nullptr;
+  c->host_bytes = 0;
+  HIPCHK(hipHostMalloc(&c->host, bytes, hipHostMallocDefault));
+  c->host_bytes = bytes;
+  return GM_OK;
+}
+
+int allreduce(gm_ctx* c, double* buf, int64_t n, hipStream_t s) {
+  if (c->comm) {
+    ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclDouble, ncclSum, c->comm, s);
+    if (r != ncclSuccess) return fail(GM_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+    return GM_OK;
+  }
+  if (c->ar_fn) {
+    if (c->ar_fn(c->ar_user, buf, n, (void*)s) != 0)
+      return fail(GM_ERR_CALLBACK, "all-reduce callback failed");
+  }
+  return GM_OK;
+}
+
+// Streaming-pass tile for K rows.
+bool pick_cfg(int64_t K, int V, PassCfg* cfg) {
+  int lpr, r;
+  if (K <= 16) { lpr = 64; r = 1; }
+  else if (K <= 32) { lpr = 64; r = 2; }
+  else if (K <= 64) { lpr = 64; r = 4; }
+  else if (K <= 128) { lpr = 32; r = 4; }
+  else if (K <= 256) { lpr = 16; r = 4; }
+  else if (K <= 512) { lpr = 8; r = 4; }
+  else if (K <= 1024) { lpr = 8; r = 8; }
+  else if (K <= 2048) { lpr = 8; r = 16; }
+  else return false;
+  *cfg = PassCfg{V, lpr, r};
+  return true;
+}
+
+int pick_vec(const float* X, int64_t d, int64_t ldx) {
+  const uintptr_t p = reinterpret_cast<uintptr_t>(X);
+  if (d % 4 == 0 && ldx % 4 == 0 && p % 16 == 0) return 4;
+  if (d % 2 == 0 && ldx % 2 == 0 && p % 8 == 0) return 2;
+  return 1;
+}
+
+int record_pass_begin(gm_ctx* c, hipStream_t s, hipEvent_t* e0, hipEvent_t* e1) {
+  *e0 = *e1 = nullptr;
+  if (!c->timing) return GM_OK;
+  for (int i = 0; i < 2; ++i) {
+    hipEvent_t e;
+    if (!c->ev_free.empty()) {
+      e = c->ev_free.back();
+      c->ev_free.pop_back();
+    } else {
+      HIPCHK(hipEventCreate(&e));
+    }
+    (i == 0 ? *e0 : *e1) = e;
+  }
+  HIPCHK(hipEventRecord(*e0, s));
+  return GM_OK;
+}
+
+int record_pass_end(gm_ctx* c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  if (!c->timing) return GM_OK;
+  HIPCHK(hipEventRecord(e1, s));
+  c->ev_used.emplace_back(e0, e1);
+  return GM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gm_last_error(void) { return g_err.c_str(); }
+int gm_abi_version(void) { return GMAGG_ABI_VERSION; }
+
+int gm_ctx_create(int device, gm_ctx** out) {
+  if (!out) return fail(GM_ERR_INVALID, "gm_ctx_create: out is NULL");
+  *out = nullptr;
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n)
+    return fail(GM_ERR_INVALID, "gm_ctx_create: device %d of %d", device, n);
+  gm_ctx* c = new gm_ctx();
+  c->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    c->num_cu = prop.multiProcessorCount;
+  *out = c;
+  return GM_OK;
+}
+
+int gm_ctx_destroy(gm_ctx* c) {
+  if (!c) return GM_OK;
+  (void)hipSetDevice(c->device);
+  if (c->comm) ncclCommDestroy(c->comm);
+  if (c->ws) (void)hipFree(c->ws);
+  if (c->host) (void)hipHostFree(c->host);
+  for (auto e : c->ev_free) (void)hipEventDestroy(e);
+  for (auto& p : c->ev_used) {
+    (void)hipEventDestroy(p.first);
+    (void)hipEventDestroy(p.second);
+  }
+  delete c;
+  return GM_OK;
+}
+
+int gm_ctx_set_shard(gm_ctx* c, int64_t d_total, int64_t d_offset) {
+  if (!c || d_total < -1 || d_offset < 0) return fail(GM_ERR_INVALID, "gm_ctx_set_shard: bad args");
+  c->d_total = d_total;
+  c->d_offset = d_offset;
+  return GM_OK;
+}
+
+int gm_ctx_set_allreduce(gm_ctx* c, gm_allreduce_cb fn, void* user) {
+  if (!c) return fail(GM_ERR_INVALID, "gm_ctx_set_allreduce: ctx is NULL");
+  c->ar_fn = fn;
+  c->ar_user = user;
+  return GM_OK;
+}
+
+int gm_rccl_get_unique_id(void* uid) {
+  if (!uid) return fail(GM_ERR_INVALID, "gm_rccl_get_unique_id: NULL");
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return fail(GM_ERR_COMM, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+  memcpy(uid, &id, sizeof id);
+  return GM_OK;
+}
+
+int gm_ctx_init_rccl(gm_ctx* c, const void* uid, int nranks, int rank) {
+  if (!c || !uid || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(GM_ERR_INVALID, "gm_ctx_init_rccl: bad args");
+  HIPCHK(hipSetDevice(c->device));
+  ncclUniqueId id;
+  memcpy(&id, uid, sizeof id);
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+  if (r != ncclSuccess) {
+    c->comm = nullptr;
+    return fail(GM_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  }
+  return GM_OK;
+}
+
+int gm_ctx_pass_timing(gm_ctx* c, int enable, double* total_ms, int64_t* launches) {
+  if (!c) return fail(GM_ERR_INVALID, "gm_ctx_pass_timing: ctx is NULL");
+  double tot = 0.0;
+  int64_t n = 0;
+  for (auto& p : c->ev_used) {
+    HIPCHK(hipEventSynchronize(p.second));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, p.first, p.second));
+    tot += ms;
+    ++n;
+    c->ev_free.push_back(p.first);
+    c->ev_free.push_back(p.second);
+  }
+  c->ev_used.clear();
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = n;
+  c->timing = enable != 0;
+  return GM_OK;
+}
+
+int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
+                     const float* guess0, float* out, const gm_opts* o, gm_result* res,
+                     void* stream) {
+  if (!c || !o || !out || !guess0) return fail(GM_ERR_INVALID, "gm_weiszfeld_f32: NULL argument");
+  if (K < 1 || d < 1 || ldx < d || (!X)) return fail(GM_ERR_INVALID, "gm_weiszfeld_f32: bad shape K=%lld d=%lld ldx=%lld", (long long)K, (long long)d, (long long)ldx);
+  if (o->maxiter < 0) return fail(GM_ERR_INVALID, "gm_weiszfeld_f32: maxiter < 0");
+  if (o->mode != GM_MODE_IDEAL && o->mode != GM_MODE_AIRCOMP)
+    return fail(GM_ERR_INVALID, "gm_weiszfeld_f32: unknown mode %d", o->mode);
+  if (o->mode == GM_MODE_AIRCOMP && o->noise_source == GM_NOISE_HOST && !o->noise_cb)
+    return fail(GM_ERR_INVALID, "gm_weiszfeld_f32: GM_NOISE_HOST needs noise_cb");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t d_total = c->d_total > 0 ? c->d_total : d;
+  const int64_t col_off = c->d_total > 0 ? c->d_offset : 0;
+  gm_result r{};
+  if (o->maxiter == 0) {
+    HIPCHK(hipMemcpyAsync(out, guess0, sizeof(float) * d, hipMemcpyDeviceToDevice, s));
+    r.last_movement = NAN;
+    if (res) *res = r;
+    return GM_OK;
+  }
+
+  // Algorithm and tile.
+  PassCfg cfg{};
+  int algo = o->algo;
+  const int V = pick_vec(X, d, ldx);
+  if (algo == GM_ALGO_AUTO || algo == GM_ALGO_STREAM) {
+    if (pick_cfg(K, V, &cfg)) algo = GM_ALGO_STREAM;
+    else if (algo == GM_ALGO_STREAM)
+      return fail(GM_ERR_UNSUPPORTED, "streaming pass supports K <= 2048 (K=%lld)", (long long)K);
+    else algo = GM_ALGO_TWOPASS;
+  }
+  if (algo == GM_ALGO_GRAM) return fail(GM_ERR_UNSUPPORTED, "Gram variant not in this build");
+  if (algo != GM_ALGO_STREAM && algo != GM_ALGO_TWOPASS)
+    return fail(GM_ERR_INVALID, "unknown algo %d", o->algo);
+
+  int nb_step, nb_init;
+  if (algo == GM_ALGO_STREAM) {
+    const int J = cfg.LPR * cfg.V;
+    const int64_t nch = (d + J - 1) / J;
+    const int64_t cap_s = (int64_t)c->num_cu * pass_blocks_per_cu(cfg, false);
+    const int64_t cap_i = (int64_t)c->num_cu * pass_blocks_per_cu(cfg, true);
+    nb_step = (int)std::max<int64_t>(1, std::min(nch, cap_s));
+    nb_init = (int)std::max<int64_t>(1, std::min(nch, cap_i));
+  } else {
+    nb_step = nb_init = twopass_blocks(K, d, c->num_cu);
+  }
+  const int nb = std::max(nb_step, nb_init);
+  Workspace w;
+  int rc = ensure_ws(c, K, d, nb, &w);
+  if (rc) return rc;
+  const bool host_noise = o->mode == GM_MODE_AIRCOMP && o->noise_source == GM_NOISE_HOST;
+  rc = ensure_host(c, sizeof(KState) + sizeof(float) * (2 * K + d_total + 1) + 256);
+  if (rc) return rc;
+  KState* hst = reinterpret_cast<KState*>(c->host);
+  float* h_hr = reinterpret_cast<float*>(c->host + align_up(sizeof(KState), 256));
+  float* h_hi = h_hr + K;
+  float* h_n = h_hi + K;   // d_total + 1
+  HIPCHK(hipMemsetAsync(w.st, 0, sizeof(KState), s));
+
+  const int noise_kind = o->mode != GM_MODE_AIRCOMP || !o->has_noise ? 0 : (host_noise ? 2 : 1);
+  const double noise_sd = std::sqrt(std::max(0.0, o->noise_var) / 2.0);
+  KspaceArgs ka{};
+  ka.K = K;
+  ka.d_total = d_total;
+  ka.mode = o->mode;
+  ka.has_noise = o->mode == GM_MODE_AIRCOMP && o->has_noise;
+  ka.noise_src = host_noise ? 1 : 0;
+  ka.tol = (float)o->tol;
+  ka.eps = (float)o->eps;
+  ka.P_max = o->P_max;
+  ka.noise_sd = noise_sd;
+  ka.seed = o->seed;
+  ka.sums = w.sums;
+  ka.r = w.r;
+  ka.h_re = w.h_re;
+  ka.h_im = w.h_im;
+  ka.n_last = w.hnoise + d;
+  ka.coef = w.coef;
+  ka.st = w.st;
+
+  auto upload_draws = [&](int64_t it) -> int {
+    // The reference's draws of iteration `it` (OMA2, M:401-402, M:411).
+    if (o->noise_cb(o->noise_user, it, h_hr, h_hi, o->has_noise ? h_n : nullptr) != 0)
+      return fail(GM_ERR_CALLBACK, "noise callback failed at iteration %lld", (long long)it);
+    HIPCHK(hipMemcpyAsync(w.h_re, h_hr, sizeof(float) * K, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(w.h_im, h_hi, sizeof(float) * K, hipMemcpyHostToDevice, s));
+    if (o->has_noise) {
+      HIPCHK(hipMemcpyAsync(w.hnoise, h_n + col_off, sizeof(float) * d, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(w.hnoise + d, h_n + d_total, sizeof(float), hipMemcpyHostToDevice, s));
+    }
+    return GM_OK;
+  };
+  auto poll = [&](KState* dst) -> int {
+    HIPCHK(hipMemcpyAsync(dst, w.st, sizeof(KState), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return GM_OK;
+  };
+
+  // Pass over X: INIT (t = -1) or STEP t; leaves the reduced partials in w.sums.
+  auto do_pass = [&](int64_t t) -> int {
+    const bool init = t < 0;
+    const float* g_old = init ? guess0 : (t == 0 ? guess0 : w.g[(t - 1) & 1]);
+    float* g_new = init ? nullptr : w.g[t & 1];
+    const int64_t S = init ? 2 * K + 2 : K + 2;
+    hipEvent_t e0, e1;
+    int rc2 = init ? GM_OK : record_pass_begin(c, s, &e0, &e1);
+    if (rc2) return rc2;
+    if (algo == GM_ALGO_STREAM) {
+      PassArgs a{};
+      a.X = X; a.K = K; a.d = d; a.ldx = ldx;
+      a.g_old = g_old; a.g_new = g_new; a.coef = w.coef; a.st = w.st;
+      a.slab = w.slab; a.slab_stride = S;
+      a.noise = noise_kind; a.hnoise = w.hnoise; a.seed = o->seed; a.iter = t; a.col_off = col_off;
+      HIPCHK(launch_pass(cfg, init, init ? nb_init : nb_step, a, s));
+      if (!init) { rc2 = record_pass_end(c, s, e0, e1); if (rc2) return rc2; }
+      HIPCHK(launch_slab_reduce(w.slab, init ? nb_init : nb_step, S, w.sums, w.st, s));
+    } else {
+      HIPCHK(launch_twopass(init, X, K, d, ldx, g_old, g_new, w.coef, w.st, noise_kind, w.hnoise,
+                            o->seed, t, col_off, w.slab, nb, w.sums, s));
+      if (!init) { rc2 = record_pass_end(c, s, e0, e1); if (rc2) return rc2; }
+    }
+    return allreduce(c, w.sums, S, s);
+  };
+
+  // Initial distances (and ||x_k||^2, ||g0||^2), then iteration-0 coefficients.
+  rc = do_pass(-1);
+  if (rc) return rc;
+  ka.t = -1;
+  ka.do_check = 0;
+  if (host_noise) { rc = upload_draws(0); if (rc) return rc; }
+  ka.do_coef = 1;
+  HIPCHK(launch_kspace(ka, s));
+
+  int check_every = o->check_every;
+  if (check_every <= 0) check_every = (K * d >= (int64_t)1 << 24) ? 1 : 16;
+  if (host_noise) check_every = 1;
+
+  int64_t t = 0;
+  for (; t < o->maxiter; ++t) {
+    rc = do_pass(t);
+    if (rc) return rc;
+    const bool last = t + 1 == o->maxiter;
+    ka.t = t;
+    if (host_noise) {
+      // tol test first; draw the next iteration only if the loop goes on (M:145-159)
+      ka.do_check = 1;
+      ka.do_coef = 0;
+      HIPCHK(launch_kspace(ka, s));
+      rc = poll(hst);
+      if (rc) return rc;
+      if (hst->done || last) break;
+      rc = upload_draws(t + 1);
+      if (rc) return rc;
+      ka.do_check = 0;
+      ka.do_coef = 1;
+      HIPCHK(launch_kspace(ka, s));
+      continue;
+    }
+    ka.do_check = 1;
+    ka.do_coef = last ? 0 : 1;
+    HIPCHK(launch_kspace(ka, s));
+    if (last || (t + 1) % check_every == 0) {
+      rc = poll(hst);
+      if (rc) return rc;
+      if (hst->done) break;
+    }
+  }
+  rc = poll(hst);
+  if (rc) return rc;
+  r.iters = hst->iters;
+  r.last_movement = hst->last_movement;
+  r.converged = hst->converged;
+  r.algo_used = algo;
+  if (r.iters < 1) return fail(GM_ERR_HIP, "Weiszfeld loop recorded no iteration");
+  HIPCHK(hipMemcpyAsync(out, w.g[(r.iters - 1) & 1], sizeof(float) * d, hipMemcpyDeviceToDevice, s));
+  if (res) *res = r;
+  return GM_OK;
+}
+
+int gm_oma_philox_f32(gm_ctx* c, float* X, int64_t K, int64_t d, int64_t ldx, double noise_var,
+                      uint64_t seed, void* stream) {
+  if (!c || !X || K < 0 || d < 0 || ldx < d || noise_var < 0)
+    return fail(GM_ERR_INVALID, "gm_oma_philox_f32: bad args");
+  if (K == 0 || d == 0) return GM_OK;
+  HIPCHK(hipSetDevice(c->device));
+  const int64_t d_total = c->d_total > 0 ? c->d_total : d;
+  const int64_t col_off = c->d_total > 0 ? c->d_offset : 0;
+  HIPCHK(launch_oma_philox(X, K, d, ldx, d_total, col_off, (float)std::sqrt(noise_var), seed,
+                           reinterpret_cast<hipStream_t>(stream)));
+  return GM_OK;
+}
+
+int gm_oma_apply_f32(gm_ctx* c, float* X, int64_t K, int64_t d, int64_t ldx, const float* hr,
+                     const float* hi, const float* nr, const float* ni, void* stream) {
+  if (!c || !X || !hr || !hi || !nr || !ni || K < 0 || d < 0 || ldx < d)
+    return fail(GM_ERR_INVALID, "gm_oma_apply_f32: bad args");
+  if (K == 0 || d == 0) return GM_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(launch_oma_apply(X, K, d, ldx, hr, hi, nr, ni, reinterpret_cast<hipStream_t>(stream)));
+  return GM_OK;
+}
+
+int gm_fill_clients_f32(gm_ctx* c, float* X, int64_t K, int64_t d, int64_t ldx, int64_t B,
+                        float mu_h, float sd_h, float mu_b, float sd_b, uint64_t seed,
+                        void* stream) {
+  if (!c || !X || K < 0 || d < 0 || ldx < d || B < 0 || B > K)
+    return fail(GM_ERR_INVALID, "gm_fill_clients_f32: bad args");
+  if (K == 0 || d == 0) return GM_OK;
+  HIPCHK(hipSetDevice(c->device));
+  const int64_t d_total = c->d_total > 0 ? c->d_total : d;
+  const int64_t col_off = c->d_total > 0 ? c->d_offset : 0;
+  HIPCHK(launch_fill_clients(X, K, d, ldx, B, mu_h, sd_h, mu_b, sd_b, d_total, col_off, seed,
+                             reinterpret_cast<hipStream_t>(stream)));
+  return GM_OK;
+}
+
+int gm_fill_normal_f32(gm_ctx* c, float* v, int64_t n, float mu, float sd, uint64_t seed,
+                       void* stream) {
+  if (!c || !v || n < 0) return fail(GM_ERR_INVALID, "gm_fill_normal_f32: bad args");
+  if (n == 0) return GM_OK;
+  HIPCHK(hipSetDevice(c->device));
+  const int64_t col_off = c->d_total > 0 ? c->d_offset : 0;
+  HIPCHK(launch_fill_normal(v, n, mu, sd, col_off, seed, reinterpret_cast<hipStream_t>(stream)));
+  return GM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+// Internal interface between the C-ABI layer (api.hip) and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gmk {
+
+constexpr int kTPB = 1024;           // threads per block of the streaming pass
+constexpr int kWaves = kTPB / 64;
+
+// Device-resident state of one Weiszfeld call (written by kspace_step, read by
+// every kernel's early-exit test and by the host poll).
+struct alignas(64) KState {
+  int32_t done;          // 1 once the tol test fired (later launches are no-ops)
+  int32_t converged;
+  int64_t iters;         // loop bodies executed
+  double last_movement;  // fp32 movement of the last body, widened
+  float a_noise;         // scale of the per-column noise in the next pass (AIRCOMP)
+  float s;               // scaler sqrt(mean(g^2)) of the current iterate (AIRCOMP)
+  double pad[4];
+};
+
+// Streaming pass configuration: V floats per lane per row, LPR lanes per row
+// segment (chunk width J = LPR*V columns), R rows per thread.
+struct PassCfg {
+  int V, LPR, R;
+};
+
+struct PassArgs {
+  const float* X;
+  int64_t K, d, ldx;
+  const float* g_old;     // iterate t (INIT: the initial guess)
+  float* g_new;           // iterate t+1 (STEP)
+  const float* coef;      // K normalised weights / AirComp coefficients (STEP)
+  const KState* st;
+  double* slab;           // [gridDim.x][slab_stride] per-block partial sums
+  int64_t slab_stride;
+  // additive column noise of the AirComp variant (STEP)
+  int noise;              // 0 none, 1 Philox, 2 host-supplied column draws
+  const float* hnoise;    // noise == 2: local column draws (d floats)
+  uint64_t seed;
+  int64_t iter;           // Weiszfeld iteration index the pass computes
+  int64_t col_off;        // global index of local column 0 (d-sharding)
+};
+
+struct KspaceArgs {
+  int64_t K, d_total, t;  // t = pass just completed, -1 after the initial pass
+  int mode;               // gm_mode
+  int has_noise, noise_src;
+  float tol, eps;
+  double P_max, noise_sd; // noise_sd = sqrt(noise_var / 2) (OMA2, M:410)
+  uint64_t seed;
+  int do_check, do_coef;
+  const double* sums;     // reduced partials (all shards)
+  double* r;              // ||x_k||^2, saved at init (AIRCOMP)
+  const float* h_re;      // host-noise draws of iteration t+1 (device copies)
+  const float* h_im;
+  const float* n_last;    // the denominator's noise element
+  float* coef;
+  KState* st;
+};
+
+// Launchers (weiszfeld.hip).  Return hipError_t.
+hipError_t launch_pass(const PassCfg& cfg, bool init, int grid, const PassArgs& a, hipStream_t s);
+int pass_blocks_per_cu(const PassCfg& cfg, bool init);
+hipError_t launch_slab_reduce(const double* slab, int nb, int64_t S, double* sums,
+                              const KState* st, hipStream_t s);
+hipError_t launch_kspace(const KspaceArgs& a, hipStream_t s);
+hipError_t launch_twopass(bool init, const float* X, int64_t K, int64_t d, int64_t ldx,
+                          const float* g_old, float* g_new, const float* coef, const KState* st,
+                          int noise, const float* hnoise, uint64_t seed, int64_t iter,
+                          int64_t col_off, double* slab, int nb, double* sums, hipStream_t s);
+int twopass_blocks(int64_t K, int64_t d, int num_cu);
+
+// OMA / synthetic fills (oma.hip).
+hipError_t launch_oma_apply(float* X, int64_t K, int64_t d, int64_t ldx, const float* hr,
+                            const float* hi, const float* nr, const float* ni, hipStream_t s);
+hipError_t launch_oma_philox(float* X, int64_t K, int64_t d, int64_t ldx, int64_t d_total,
+                             int64_t col_off, float sd, uint64_t seed, hipStream_t s);
+hipError_t launch_fill_clients(float* X, int64_t K, int64_t d, int64_t ldx, int64_t B,
+                               float mu_h, float sd_h, float mu_b, float sd_b, int64_t d_total,
+                               int64_t col_off, uint64_t seed, hipStream_t s);
+hipError_t launch_fill_normal(float* v, int64_t n, float mu, float sd, int64_t off,
+                              uint64_t seed, hipStream_t s);
+
+}  // namespace gmk

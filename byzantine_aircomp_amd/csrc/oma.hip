@@ -1,0 +1,127 @@
+// OMA per-client pre-noise (MNIST_Air_weight.py:385-394) and the seeded
+// synthetic client-update generator used by the benchmark.
+//
+// OMA:  X[k, j] += (h_re[k] * n_re[k, j] + h_im[k] * n_im[k, j]) / (h_re[k]^2 + h_im[k]^2)
+// One read + one write of X (8 B per element); the draws either come from the
+// caller (the reference's own CPU-generator values, bit-exact) or from Philox.
+#include "gmagg_internal.h"
+#include "philox.h"
+
+namespace gmk {
+
+// Host-injected draws.  fp contraction is off so the fp32 op order is the
+// reference's: mul, mul, add, mul, mul, add, div, add (M:393-394).
+__global__ void __launch_bounds__(256) oma_apply(float* __restrict__ X, int64_t K, int64_t d,
+                                                 int64_t ldx, const float* __restrict__ hr,
+                                                 const float* __restrict__ hi,
+                                                 const float* __restrict__ nr,
+                                                 const float* __restrict__ ni) {
+#pragma clang fp contract(off)
+  const int64_t n = K * d;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = e / d, j = e - k * d;
+    const float a = hr[k], b = hi[k];
+    const float num = a * nr[e] + b * ni[e];
+    const float den = a * a + b * b;
+    float* p = X + k * ldx + j;
+    *p = *p + num / den;
+  }
+}
+
+// Philox draws: h_k ~ CN(0, 1) per client, n_re/n_im ~ N(0, var) per element
+// keyed by the element's global index k * d_total + (col_off + j).
+__global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t K, int64_t d,
+                                                  int64_t ldx, int64_t d_total, int64_t col_off,
+                                                  float sd, uint64_t seed) {
+  const int64_t n = K * d;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = e / d, j = e - k * d;
+    float h[4], z[4];
+    normal4(seed, kStreamOmaChannel, 0, (uint64_t)k, h);
+    const float a = h[0] * 0.70710678118654752f, b = h[1] * 0.70710678118654752f;
+    normal4(seed, kStreamOmaNoise, 0, (uint64_t)(k * d_total + col_off + j), z);
+    const float num = a * (sd * z[0]) + b * (sd * z[1]);
+    float* p = X + k * ldx + j;
+    *p = *p + num / (a * a + b * b);
+  }
+}
+
+// Synthetic client updates: honest rows ~ N(mu_h, sd_h^2), the
+// last B rows ~ N(mu_b, sd_b^2).  Element (k, global column c) uses normal
+// (c & 3) of Philox block (k, c >> 2), so any shard reproduces its columns.
+__global__ void __launch_bounds__(256) fill_clients(float* __restrict__ X, int64_t K, int64_t d,
+                                                    int64_t ldx, int64_t B, float mu_h,
+                                                    float sd_h, float mu_b, float sd_b,
+                                                    int64_t col_off, uint64_t seed) {
+  const int64_t groups = (d + 3) / 4;
+  const int64_t n = K * groups;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = e / groups, g = e - k * groups;
+    const bool byz = k >= K - B;
+    const float mu = byz ? mu_b : mu_h, sd = byz ? sd_b : sd_h;
+    float* row = X + k * ldx;
+    float z[4];
+    int64_t cached = -1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = g * 4 + u;
+      if (j >= d) break;
+      const int64_t c = col_off + j;
+      if ((c >> 2) != cached) {
+        cached = c >> 2;
+        normal4(seed, kStreamFill, (uint64_t)k, (uint64_t)cached, z);
+      }
+      row[j] = mu + sd * z[c & 3];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) fill_normal(float* __restrict__ v, int64_t n, float mu,
+                                                   float sd, int64_t off, uint64_t seed) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = off + i;
+    float z[4];
+    normal4(seed, kStreamFill, 0xFFFFFFFFull, (uint64_t)(c >> 2), z);
+    v[i] = mu + sd * z[c & 3];
+  }
+}
+
+static int grid_for(int64_t n) {
+  const int64_t g = (n + 255) / 256;
+  return (int)(g < 65536 ? (g > 0 ? g : 1) : 65536);
+}
+
+hipError_t launch_oma_apply(float* X, int64_t K, int64_t d, int64_t ldx, const float* hr,
+                            const float* hi, const float* nr, const float* ni, hipStream_t s) {
+  hipLaunchKernelGGL(oma_apply, dim3(grid_for(K * d)), dim3(256), 0, s, X, K, d, ldx, hr, hi, nr,
+                     ni);
+  return hipGetLastError();
+}
+
+hipError_t launch_oma_philox(float* X, int64_t K, int64_t d, int64_t ldx, int64_t d_total,
+                             int64_t col_off, float sd, uint64_t seed, hipStream_t s) {
+  hipLaunchKernelGGL(oma_philox, dim3(grid_for(K * d)), dim3(256), 0, s, X, K, d, ldx, d_total,
+                     col_off, sd, seed);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_clients(float* X, int64_t K, int64_t d, int64_t ldx, int64_t B,
+                               float mu_h, float sd_h, float mu_b, float sd_b, int64_t d_total,
+                               int64_t col_off, uint64_t seed, hipStream_t s) {
+  (void)d_total;
+  hipLaunchKernelGGL(fill_clients, dim3(grid_for(K * ((d + 3) / 4))), dim3(256), 0, s, X, K, d,
+                     ldx, B, mu_h, sd_h, mu_b, sd_b, col_off, seed);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_normal(float* v, int64_t n, float mu, float sd, int64_t off, uint64_t seed,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(fill_normal, dim3(grid_for(n)), dim3(256), 0, s, v, n, mu, sd, off, seed);
+  return hipGetLastError();
+}
+
+}  // namespace gmk

@@ -1,0 +1,81 @@
+// Counter-based Philox4x32-10 + Box-Muller normals for the AirComp channel.
+//
+// Every draw is a pure function of (seed, stream, iteration, global index), so
+// d-shards regenerate identical channel coefficients h_k and identical noise
+// columns without communicating, and a launch can be replayed.  Streams keep
+// the reference's draw families apart (OMA2 M:401-402 / M:411, OMA M:389-392).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gmk {
+
+enum : uint32_t {
+  kStreamChannel = 0x43484E4Cu,   // OMA2 h_re/h_im per client, per iteration
+  kStreamNoise = 0x4E4F4953u,     // OMA2 additive noise per column, per iteration
+  kStreamOmaChannel = 0x4F4D4143u,
+  kStreamOmaNoise = 0x4F4D414Eu,
+  kStreamFill = 0x46494C4Cu,      // synthetic client updates
+};
+
+struct u4 { uint32_t x, y, z, w; };
+
+__host__ __device__ __forceinline__ uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t* hi) {
+  uint64_t p = (uint64_t)a * (uint64_t)b;
+  *hi = (uint32_t)(p >> 32);
+  return (uint32_t)p;
+}
+
+// Philox4x32 with 10 rounds (Salmon et al., SC'11).
+__host__ __device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0, hi1;
+    uint32_t lo0 = mulhilo(0xD2511F53u, c.x, &hi0);
+    uint32_t lo1 = mulhilo(0xCD9E8D57u, c.z, &hi1);
+    c = u4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// (0, 1] uniform from 32 random bits, never 0 so log() is finite.
+__host__ __device__ __forceinline__ float u01(uint32_t v) {
+  return ((float)(v >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+// Two independent standard normals from two uniform words (Box-Muller).
+__host__ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float* n0, float* n1) {
+  float r = sqrtf(-2.0f * logf(u01(a)));
+  float t = 6.283185307179586f * u01(b);
+  float s, c;
+#ifdef __HIP_DEVICE_COMPILE__
+  __sincosf(t, &s, &c);
+#else
+  s = sinf(t); c = cosf(t);
+#endif
+  *n0 = r * c;
+  *n1 = r * s;
+}
+
+// Four standard normals for counter (idx, iter) on `stream`.
+__host__ __device__ __forceinline__ void normal4(uint64_t seed, uint32_t stream, uint64_t iter,
+                                                 uint64_t idx, float out[4]) {
+  u4 c{(uint32_t)idx, (uint32_t)(idx >> 32), (uint32_t)iter, stream ^ (uint32_t)(iter >> 32)};
+  u4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  box_muller(r.x, r.y, &out[0], &out[1]);
+  box_muller(r.z, r.w, &out[2], &out[3]);
+}
+
+// One standard normal for element `idx` (uses half of a Philox block).
+__host__ __device__ __forceinline__ float normal1(uint64_t seed, uint32_t stream, uint64_t iter,
+                                                  uint64_t idx) {
+  u4 c{(uint32_t)idx, (uint32_t)(idx >> 32), (uint32_t)iter, stream ^ (uint32_t)(iter >> 32)};
+  u4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  float n0, n1;
+  box_muller(r.x, r.y, &n0, &n1);
+  return n0;
+}
+
+}  // namespace gmk

@@ -1,0 +1,158 @@
+/*
+ * gmagg.h — C ABI of the MI355X geometric-median aggregation library
+ * (libgmagg.so, built from byzantine_aircomp_amd/csrc/ for gfx950).
+ *
+ * This is the drop-in boundary for the reference's aggregation call
+ *     weight_vector = aggregate(weight_f, options)          MNIST_Air_weight.py:353
+ * with aggregate resolved by eval(args.agg) (MNIST_Air_weight.py:580).  Each entry
+ * point below names the reference function it replaces.  Plain pointers and
+ * sizes only: no torch types cross this boundary.
+ *
+ * Conventions
+ *   - Every call returns 0 (GM_OK) or a negative GM_ERR_* code; the message of
+ *     the last failure on the calling thread is gm_last_error().  Nothing aborts
+ *     or throws across the ABI.
+ *   - Device pointers are HIP device pointers on the context's device; the
+ *     caller owns X / guess / out, the library owns its workspace.
+ *   - Work is stream-ordered on `stream` (a hipStream_t passed as void*; NULL =
+ *     the default stream).  gm_weiszfeld_f32 blocks only to learn whether the
+ *     iteration has converged; the OMA entry points never block.
+ *   - A context is used by one host thread at a time.
+ *
+ * Layout: X is row-major [K][ldx] fp32, row k = client k's flattened update
+ * (model.parameters() order, MNIST_Air_weight.py:206-209), ldx >= d.
+ */
+#ifndef GMAGG_H
+#define GMAGG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GMAGG_ABI_VERSION 1
+
+enum gm_status {
+    GM_OK = 0,
+    GM_ERR_INVALID = -1,      /* bad argument (null pointer, negative size, ...) */
+    GM_ERR_HIP = -2,          /* a HIP runtime call failed */
+    GM_ERR_UNSUPPORTED = -3,  /* shape / mode this build does not handle */
+    GM_ERR_CALLBACK = -4,     /* a user callback (noise, all-reduce) returned non-zero */
+    GM_ERR_COMM = -5          /* RCCL failure */
+};
+
+enum gm_mode {
+    GM_MODE_IDEAL = 0,        /* gm2: MNIST_Air_weight.py:162-184 */
+    GM_MODE_AIRCOMP = 1       /* gm + OMA2 per iteration: MNIST_Air_weight.py:131-160, 396-414 */
+};
+
+enum gm_noise_source {
+    GM_NOISE_PHILOX = 0,      /* on-device Philox4x32-10, keyed (seed, iteration, global index) */
+    GM_NOISE_HOST = 1         /* caller supplies the reference's draws through noise_cb */
+};
+
+enum gm_algo {
+    GM_ALGO_AUTO = 0,
+    GM_ALGO_STREAM = 1,       /* fused one-read-per-iteration streaming Weiszfeld */
+    GM_ALGO_TWOPASS = 2,      /* two reads per iteration; any K */
+    GM_ALGO_GRAM = 3          /* K x K Gram on MFMA, iterations in K-space (IDEAL only) */
+};
+
+/* Host-noise callback for GM_NOISE_HOST: fill the draws of Weiszfeld iteration
+ * `iter` (0-based), exactly as OMA2 draws them (MNIST_Air_weight.py:401-402, 411):
+ * h_re[K], h_im[K] ~ N(0, 1/2) and, when the options ask for noise,
+ * noise[d_total + 1] ~ N(0, noise_var / 2) (the last element is the
+ * denominator's).  Buffers are host memory owned by the library.  Return 0. */
+typedef int (*gm_noise_cb)(void* user, int64_t iter, float* h_re, float* h_im, float* noise);
+
+/* Optional d-sharding hook: sum `count` doubles in place across all shards,
+ * stream-ordered on `stream`.  Return 0.  (gm_ctx_init_rccl installs a native
+ * RCCL all-reduce instead.) */
+typedef int (*gm_allreduce_cb)(void* user, double* dev_buf, int64_t count, void* stream);
+
+typedef struct gm_opts {
+    int64_t maxiter;          /* options['maxiter'], reference default 200 (M:136, M:167) */
+    double tol;               /* options['tol'], default 1e-5; compared as fp32 like the reference */
+    double eps;               /* distance floor, 1e-4 in the reference (M:151, M:178) */
+    int32_t mode;             /* gm_mode */
+    int32_t has_noise;        /* AIRCOMP: options['noise_var'] is not None */
+    double noise_var;         /* AIRCOMP: channel-noise variance (OMA2 std = sqrt(var/2), M:410) */
+    double P_max;             /* AIRCOMP: options['P_max'], default 1 (M:136) */
+    uint64_t seed;            /* GM_NOISE_PHILOX key */
+    int32_t noise_source;     /* gm_noise_source */
+    int32_t algo;             /* gm_algo */
+    gm_noise_cb noise_cb;     /* GM_NOISE_HOST */
+    void* noise_user;
+    int32_t check_every;      /* host convergence poll interval in iterations; 0 = auto */
+    int32_t reserved;
+} gm_opts;
+
+typedef struct gm_result {
+    int64_t iters;            /* Weiszfeld loop bodies executed (M:145 / M:173) */
+    double last_movement;     /* ||guess_t - guess_{t+1}|| of the last body (M:156 / M:180) */
+    int32_t converged;        /* 1 if the loop exited through the tol test */
+    int32_t algo_used;        /* gm_algo actually run */
+} gm_result;
+
+typedef struct gm_ctx gm_ctx;
+
+/* Context: device binding, workspace, optional shard description. */
+int gm_ctx_create(int device, gm_ctx** out);
+int gm_ctx_destroy(gm_ctx* ctx);
+
+/* d-sharding: this shard holds global columns [d_offset, d_offset + d_local) of
+ * a d_total-long update; per-iteration partial sums go through the all-reduce. */
+int gm_ctx_set_shard(gm_ctx* ctx, int64_t d_total, int64_t d_offset);
+int gm_ctx_set_allreduce(gm_ctx* ctx, gm_allreduce_cb fn, void* user);
+/* Native RCCL all-reduce over xGMI: `unique_id` is the 128-byte ncclUniqueId
+ * made by rank 0 (gm_rccl_get_unique_id) and shared by the caller. */
+int gm_rccl_get_unique_id(void* unique_id_128);
+int gm_ctx_init_rccl(gm_ctx* ctx, const void* unique_id_128, int nranks, int rank);
+
+/* gm2 / gm: Weiszfeld geometric median of the K rows of X.
+ * Replaces gm2(wList, options) (MNIST_Air_weight.py:162-184) with
+ * opts->mode = GM_MODE_IDEAL, and gm(wList, options) (MNIST_Air_weight.py:131-160,
+ * calling OMA2 M:396-414 each iteration) with GM_MODE_AIRCOMP.
+ * guess0 = options['guess'] (d floats); out receives the returned iterate
+ * (d floats).  maxiter == 0 copies guess0 to out. */
+int gm_weiszfeld_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t ldx,
+                     const float* guess0, float* out, const gm_opts* opts,
+                     gm_result* result, void* stream);
+
+/* OMA(message, noise_var): in-place per-client equalised AWGN
+ * (MNIST_Air_weight.py:385-394), draws from on-device Philox keyed by `seed`. */
+int gm_oma_philox_f32(gm_ctx* ctx, float* X, int64_t K, int64_t d, int64_t ldx,
+                      double noise_var, uint64_t seed, void* stream);
+
+/* OMA with the reference's own draws (device arrays): h_re[K], h_im[K],
+ * n_re[K*d], n_im[K*d] (row-major, already scaled by sqrt(noise_var)).
+ * Bit-exact with the reference's fp32 op order. */
+int gm_oma_apply_f32(gm_ctx* ctx, float* X, int64_t K, int64_t d, int64_t ldx,
+                     const float* h_re, const float* h_im, const float* n_re,
+                     const float* n_im, void* stream);
+
+/* Fill X[K][ldx] (first d columns) with seeded synthetic client updates on the
+ * device: rows k < K - B ~ N(mu_h, sd_h^2), the last B rows ~ N(mu_b, sd_b^2)
+ * (BASELINE.md §3 recipe), Philox-keyed so every shard generates its own
+ * columns of the same global matrix (global column = d_offset + j). */
+int gm_fill_clients_f32(gm_ctx* ctx, float* X, int64_t K, int64_t d, int64_t ldx, int64_t B,
+                        float mu_h, float sd_h, float mu_b, float sd_b, uint64_t seed,
+                        void* stream);
+/* Fill v[n] ~ N(mu, sd^2) (global index = d_offset + i). */
+int gm_fill_normal_f32(gm_ctx* ctx, float* v, int64_t n, float mu, float sd, uint64_t seed,
+                       void* stream);
+
+/* Timing hook for the dominant kernel: accumulated device time (ms, HIP
+ * events on the launch stream) and launch count of the fused Weiszfeld pass
+ * since the last reset. */
+int gm_ctx_pass_timing(gm_ctx* ctx, int enable, double* total_ms, int64_t* launches);
+
+const char* gm_last_error(void);
+int gm_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GMAGG_H */

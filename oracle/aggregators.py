@@ -1,0 +1,179 @@
+"""Op-for-op PyTorch-CPU restatement of the reference's aggregation path.
+
+TEST INFRASTRUCTURE ONLY (see ``oracle/__init__.py``): the checker for the HIP
+path and the timed ``cpu_baseline`` of ``bench.py``.  Never shipped, never
+called by ``byzantine_aircomp_amd``.
+
+Reference = goldenBill/Byzantine_AirComp, ``MNIST_Air_weight.py`` (cited "M:")
+— ``EMNIST_Air_weight.py`` holds the same functions at the same lines
+131-204 and ``OMA``/``OMA2`` at +2 lines.
+
+Every function keeps the reference's fp32 temporaries and op order, so on the
+same inputs and the same CPU-generator state it reproduces the reference to the
+last bit (pinned by ``tests/test_oracle_golden.py`` against fixtures made by
+importing the reference).  In addition to the aggregate, the Weiszfeld
+restatements report what the reference computes but does not return: the
+number of loop bodies executed and the last ``guess_movement``.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+import torch
+
+CLAMP = 1e-4  # M:151 / M:178 distance floor
+
+
+@dataclass
+class WeiszfeldTrace:
+    """What a Weiszfeld run did, beyond its return value."""
+
+    iters: int            # loop bodies executed (M:145 / M:173)
+    last_movement: float  # ||guess_t - guess_{t+1}|| of the final body, nan if none
+
+
+def _with_defaults(wList: torch.Tensor, options: dict, defaults: dict) -> dict:
+    # M:136-138 / M:167-169: the defaults dict is built EAGERLY, so the mean
+    # (K x d pass) is computed even when a guess is supplied.
+    merged = dict(defaults)
+    merged["guess"] = wList.mean(dim=0)
+    merged.update(options)
+    return merged
+
+
+def _clamped_row_distances(wList: torch.Tensor, guess: torch.Tensor) -> torch.Tensor:
+    # M:174 + M:178 (same as M:147 + M:151): fp32 row norms, floor 1e-4 held in
+    # an fp32 0-d tensor and applied with torch.max (NaN propagates).
+    dist = torch.norm(wList - guess, dim=1)
+    return torch.max(torch.tensor(CLAMP).to(wList.device), dist)
+
+
+def gm2(wList: torch.Tensor, options: Optional[dict] = None):
+    """Ideal Weiszfeld geometric median, M:162-184.  Returns (guess, trace)."""
+    opts = _with_defaults(wList, options or {}, {"maxiter": 200, "tol": 1e-5})
+    guess = opts["guess"]
+    n, moved = 0, float("nan")
+    for _ in range(opts["maxiter"]):
+        n += 1
+        dist = _clamped_row_distances(wList, guess)
+        nxt = (wList / dist.unsqueeze(-1)).sum(dim=0) / (1 / dist).sum()   # M:179
+        movement = (guess - nxt).norm()                                    # M:180
+        moved = float(movement)
+        guess = nxt                                                         # M:181
+        if movement <= opts["tol"]:                                        # M:182
+            break
+    return guess, WeiszfeldTrace(n, moved)
+
+
+def oma2(message: torch.Tensor, P_max=10, noise_var=None, threshold=1,
+         draw: Optional[Callable] = None) -> torch.Tensor:
+    """AirComp weighted sum with truncated channel inversion, M:396-414.
+
+    ``draw(shape, std)`` supplies the normals; default is the reference's own
+    ``torch.normal(torch.zeros(shape), std)`` on the global CPU generator, in
+    the reference's order: channel real [K], channel imag [K], noise [d+1].
+    """
+    draw = draw or (lambda shape, std: torch.normal(torch.zeros(*shape), std))
+    msg = message.clone().detach()
+    K, L = msg.shape
+    h_re = draw((K,), 1 / math.sqrt(2)).to(message.device)
+    h_im = draw((K,), 1 / math.sqrt(2)).to(message.device)
+    h2 = h_re ** 2 + h_im ** 2                                  # M:403
+    p_up = torch.max(torch.mean(msg ** 2 / h2.unsqueeze(-1), dim=-1), threshold)  # M:404-405
+    gain = torch.sqrt(P_max / p_up)                              # M:407
+    summed = (msg * gain.unsqueeze(-1)).sum(dim=0)               # M:408
+    if noise_var is None:
+        return summed                                            # M:414
+    noise = draw((L,), math.sqrt(noise_var / 2)).to(message.device)
+    return summed.add_(noise)                                    # M:409-412
+
+
+def gm(wList: torch.Tensor, options: Optional[dict] = None,
+       draw: Optional[Callable] = None):
+    """AirComp Weiszfeld geometric median, M:131-160.  Returns (guess, trace)."""
+    opts = _with_defaults(wList, options or {},
+                          {"maxiter": 200, "tol": 1e-5, "noise_var": None, "P_max": 1})
+    guess = opts["guess"]
+    n, moved = 0, float("nan")
+    for _ in range(opts["maxiter"]):
+        n += 1
+        scaler = torch.sqrt(torch.mean(guess ** 2))               # M:146
+        dist = _clamped_row_distances(wList, guess)               # M:147, M:151
+        msg = torch.cat([wList / dist.unsqueeze(-1), scaler / dist.unsqueeze(-1)], dim=-1)
+        y = oma2(msg, P_max=opts["P_max"], noise_var=opts["noise_var"],
+                 threshold=(scaler ** 2) * 500, draw=draw)        # M:152
+        nxt = y[:-1] / y[-1:] * scaler                            # M:153-155
+        movement = (guess - nxt).norm()                           # M:156
+        moved = float(movement)
+        guess = nxt
+        if movement <= opts["tol"]:                               # M:158
+            break
+    return guess, WeiszfeldTrace(n, moved)
+
+
+def oma_(message: torch.Tensor, noise_var: float = 0.01, draw: Optional[Callable] = None):
+    """Per-client equalised AWGN, applied in place, M:385-394.
+
+    Draw order (M:389-392): channel real [K,1], channel imag [K,1], noise
+    real [K,d], noise imag [K,d]; std 1/sqrt(2) for the channel and
+    sqrt(noise_var) for the noise.
+    """
+    draw = draw or (lambda shape, std: torch.normal(torch.zeros(*shape), std))
+    K, d = message.shape
+    sd = math.sqrt(noise_var)
+    h_re = draw((K, 1), 1 / math.sqrt(2)).to(message.device)
+    h_im = draw((K, 1), 1 / math.sqrt(2)).to(message.device)
+    n_re = draw((K, d), sd).to(message.device)
+    n_im = draw((K, d), sd).to(message.device)
+    message[:].add_((h_re * n_re + h_im * n_im) / (h_re ** 2 + h_im ** 2))   # M:393-394
+    return message
+
+
+# --- alternative aggregators, M:186-204 -------------------
+
+def mean(wList, options=None):
+    return torch.mean(wList, dim=0)                               # M:186-187
+
+
+def trimmed_mean(wList, options=None):
+    K = wList.shape[0]
+    b = int(K * 0.1)                                              # M:191
+    low = wList.topk(K - b, dim=0, largest=False)[0]
+    return torch.mean(low.topk(K - 2 * b, dim=0, largest=True)[0], dim=0)   # M:192
+
+
+def median(wList, options=None):
+    return wList.median(dim=0)[0]                                 # M:194-195 (lower median)
+
+
+def krum(wList, options):
+    honest = options["honestSize"]
+    d2 = ((wList.unsqueeze(1) - wList.unsqueeze(0)) ** 2).sum(dim=-1)   # M:199
+    score = d2.topk(k=honest - 1, dim=1, largest=False)[0].sum(dim=1)  # M:200-202
+    return wList[score.argmin()]                                  # M:203-204
+
+
+def variance(wList, honest):
+    """getVarience, M:127-129."""
+    h = wList[:honest]
+    return torch.mean(((h - h.mean(dim=0)) ** 2).sum(dim=1))
+
+
+# --- fp64 K-space cross-check (not op-for-op; used to bound fp32 drift) ------
+
+def gm2_f64(X: torch.Tensor, guess: torch.Tensor, maxiter: int = 200, tol: float = 1e-5):
+    """Weiszfeld in float64 on the same inputs; returns (guess_f64, trace)."""
+    X64, g = X.double(), guess.double()
+    n, moved = 0, float("nan")
+    for _ in range(maxiter):
+        n += 1
+        dist = torch.clamp(torch.linalg.vector_norm(X64 - g, dim=1), min=CLAMP)
+        w = 1.0 / dist
+        nxt = (w @ X64) / w.sum()
+        moved = float(torch.linalg.vector_norm(g - nxt))
+        g = nxt
+        if moved <= tol:
+            break
+    return g, WeiszfeldTrace(n, moved)

@@ -1,0 +1,84 @@
+"""The C-ABI library loads and exports every symbol include/gmagg.h declares.
+
+CPU only: no compute calls (there is no GPU here); calls that need a device must
+fail cleanly with a status code and a message, never crash.
+"""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+from byzantine_aircomp_amd import _lib
+
+HEADER = os.path.join(ROOT, "include", "gmagg.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(gm_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("gm_weiszfeld_f32", "gm_oma_philox_f32", "gm_oma_apply_f32", "gm_ctx_create",
+                 "gm_ctx_destroy", "gm_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    assert set(declared_functions()) == bound
+
+
+def test_exports_are_c_linkage():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    for name in declared_functions():
+        assert name in syms, f"{name} not exported with C linkage"
+
+
+def test_library_is_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _lib.LIB_PATH],
+                         capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("llvm-objdump --offloading unavailable")
+    assert "gfx950" in out.stdout + out.stderr
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """ctypes' view of gm_opts / gm_result == the C compiler's (gcc on the header)."""
+    fields = [f for f, _ in _lib.GmOpts._fields_]
+    rfields = [f for f, _ in _lib.GmResult._fields_]
+    src = ["#include <stdio.h>", "#include <stddef.h>", '#include "gmagg.h"', "int main(void){",
+           'printf("%zu\\n", sizeof(gm_opts));', 'printf("%zu\\n", sizeof(gm_result));']
+    src += [f'printf("%zu\\n", offsetof(gm_opts, {f}));' for f in fields]
+    src += [f'printf("%zu\\n", offsetof(gm_result, {f}));' for f in rfields]
+    src += ["return 0;}"]
+    (tmp_path / "layout.c").write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(tmp_path / "layout.c"),
+                    "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    want = [C.sizeof(_lib.GmOpts), C.sizeof(_lib.GmResult)]
+    want += [getattr(_lib.GmOpts, f).offset for f in fields]
+    want += [getattr(_lib.GmResult, f).offset for f in rfields]
+    assert got == want
+
+
+def test_errors_are_reported_not_raised():
+    lib = _lib.load()
+    assert lib.gm_abi_version() == _lib.ABI_VERSION
+    rc = lib.gm_weiszfeld_f32(None, None, 0, 0, 0, None, None, None, None, None)
+    assert rc == -1
+    assert b"NULL" in lib.gm_last_error()
+    rc = lib.gm_ctx_set_shard(None, 10, 0)
+    assert rc == -1
