@@ -137,19 +137,24 @@ int allreduce(gm_ctx* c, double* buf, int64_t n, hipStream_t s) {
 }
 
 // Streaming-pass tile for K rows.
-bool pick_cfg(int64_t K, int V, PassCfg* cfg) {
+// The tile is K_pad x J with J = LPR*V columns; NRG = 16*64/LPR row groups of
+// R rows each cover K.  Bigger K -> narrower chunk, so a block's tile (and the
+// bytes it has in flight) stays ~64-128 KiB.
+bool pick_cfg(int64_t K, int V, int64_t ldx, PassCfg* cfg) {
   int lpr, r;
   if (K <= 16) { lpr = 64; r = 1; }
   else if (K <= 32) { lpr = 64; r = 2; }
   else if (K <= 64) { lpr = 64; r = 4; }
-  else if (K <= 128) { lpr = 32; r = 4; }
-  else if (K <= 256) { lpr = 16; r = 4; }
-  else if (K <= 512) { lpr = 8; r = 4; }
+  else if (K <= 128) { lpr = 64; r = 8; }
+  else if (K <= 256) { lpr = 32; r = 8; }
+  else if (K <= 512) { lpr = 16; r = 8; }
   else if (K <= 1024) { lpr = 8; r = 8; }
-  else if (K <= 2048) { lpr = 8; r = 16; }
+  else if (K <= 2048) { lpr = 4; r = 8; }
   else return false;
+  // lane offsets are 32-bit: (rows per wave - 1) * ldx + ldx must fit in bytes
+  if ((uint64_t)(64 / lpr) * (uint64_t)ldx * 4u >= (1ull << 32)) return false;
   *cfg = PassCfg{V, lpr, r};
-  return true;
+  return pass_cfg_supported(*cfg);
 }
 
 int pick_vec(const float* X, int64_t d, int64_t ldx) {
@@ -306,7 +311,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   int algo = o->algo;
   const int V = pick_vec(X, d, ldx);
   if (algo == GM_ALGO_AUTO || algo == GM_ALGO_STREAM) {
-    if (pick_cfg(K, V, &cfg)) algo = GM_ALGO_STREAM;
+    if (pick_cfg(K, V, ldx, &cfg)) algo = GM_ALGO_STREAM;
     else if (algo == GM_ALGO_STREAM)
       return fail(GM_ERR_UNSUPPORTED, "streaming pass supports K <= 2048 (K=%lld)", (long long)K);
     else algo = GM_ALGO_TWOPASS;
@@ -314,13 +319,14 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   if (algo == GM_ALGO_GRAM) return fail(GM_ERR_UNSUPPORTED, "Gram variant not in this build");
   if (algo != GM_ALGO_STREAM && algo != GM_ALGO_TWOPASS)
     return fail(GM_ERR_INVALID, "unknown algo %d", o->algo);
+  const int init_mode = o->mode == GM_MODE_AIRCOMP ? 2 : 1;   // ||x_k||^2 only for AirComp
 
   int nb_step, nb_init;
   if (algo == GM_ALGO_STREAM) {
     const int J = cfg.LPR * cfg.V;
     const int64_t nch = (d + J - 1) / J;
-    const int64_t cap_s = (int64_t)c->num_cu * pass_blocks_per_cu(cfg, false);
-    const int64_t cap_i = (int64_t)c->num_cu * pass_blocks_per_cu(cfg, true);
+    const int64_t cap_s = (int64_t)c->num_cu * pass_blocks_per_cu(cfg, 0);
+    const int64_t cap_i = (int64_t)c->num_cu * pass_blocks_per_cu(cfg, init_mode);
     nb_step = (int)std::max<int64_t>(1, std::min(nch, cap_s));
     nb_init = (int)std::max<int64_t>(1, std::min(nch, cap_i));
   } else {
@@ -393,7 +399,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       a.g_old = g_old; a.g_new = g_new; a.coef = w.coef; a.st = w.st;
       a.slab = w.slab; a.slab_stride = S;
       a.noise = noise_kind; a.hnoise = w.hnoise; a.seed = o->seed; a.iter = t; a.col_off = col_off;
-      HIPCHK(launch_pass(cfg, init, init ? nb_init : nb_step, a, s));
+      HIPCHK(launch_pass(cfg, init ? init_mode : 0, init ? nb_init : nb_step, a, s));
       if (!init) { rc2 = record_pass_end(c, s, e0, e1); if (rc2) return rc2; }
       HIPCHK(launch_slab_reduce(w.slab, init ? nb_init : nb_step, S, w.sums, w.st, s));
     } else {

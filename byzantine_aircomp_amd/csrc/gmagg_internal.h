@@ -60,9 +60,12 @@ struct KspaceArgs {
   KState* st;
 };
 
-// Launchers (weiszfeld.hip).  Return hipError_t.
-hipError_t launch_pass(const PassCfg& cfg, bool init, int grid, const PassArgs& a, hipStream_t s);
-int pass_blocks_per_cu(const PassCfg& cfg, bool init);
+// Streaming pass (stream_pass.hip).  mode: 0 step, 1 init, 2 init + ||x_k||^2.
+hipError_t launch_pass(const PassCfg& cfg, int mode, int grid, const PassArgs& a, hipStream_t s);
+int pass_blocks_per_cu(const PassCfg& cfg, int mode);
+bool pass_cfg_supported(const PassCfg& cfg);
+
+// Reduction, K-space step and the two-pass path (weiszfeld.hip).
 hipError_t launch_slab_reduce(const double* slab, int nb, int64_t S, double* sums,
                               const KState* st, hipStream_t s);
 hipError_t launch_kspace(const KspaceArgs& a, hipStream_t s);

@@ -1,0 +1,306 @@
+// The fused streaming Weiszfeld pass for gfx950: ONE HBM read of X per
+// iteration.
+//
+// Reference (MNIST_Air_weight.py): gm2's loop body M:174-181 computes
+//   dist = max(1e-4, ||x_k - g||)          (a K x d read)
+//   g'   = sum_k x_k/dist_k / sum 1/dist_k (another K x d read)
+//   movement = ||g - g'||
+// and the next body starts by re-reading X for the distances to g'.  Here a
+// block owns a chunk of J columns x ALL K rows (in VGPRs) at a time:
+//   phase A  g'_j = sum_k c_k x_kj          (c_k from the K-space step: 1/dist_k
+//                                            normalised, or the AirComp gains)
+//   phase B  D_k += sum_{j in chunk} (x_kj - g'_j)^2  -- the NEXT iteration's
+//            distances, while the tile is still in registers
+// plus ||g - g'||^2 and ||g'||^2.  INIT passes compute D_k to the initial
+// guess (and ||x_k||^2 for the AirComp power control).
+//
+// Thread map (1024 threads = 16 waves): lane c of a row segment covers columns
+// [c*V, c*V+V) of the chunk, QW = 64/LPR row groups per wave, NRG = 16*QW row
+// groups per block, row group rg owns rows rg + NRG*i (i < R).  Every wave
+// instruction reads LPR*V*4 contiguous bytes of QW rows: 1 KiB per
+// instruction for V = 4.  Per-block partials go to a slab (fp64), summed by
+// slab_reduce in a fixed order: deterministic, no atomics.
+#include "device_util.h"
+#include "gmagg_internal.h"
+#include "philox.h"
+
+namespace gmk {
+
+template <int V, int R>
+struct Tile {
+  float x[R][V];
+  float g[V];    // INIT: the guess at this lane's columns
+  float gold;    // STEP finisher thread: g_t at its column
+  float hn;      // STEP finisher thread, host noise: its column's draw
+};
+
+// MODE: 0 step, 1 init, 2 init + ||x_k||^2.  PIPE: chunk c+1's loads are in
+// flight while chunk c is reduced (two tiles of registers).
+template <int V, int LPR, int R, int MODE, bool PIPE>
+__global__ void __launch_bounds__(kTPB) weiszfeld_pass(PassArgs a) {
+  constexpr bool INIT = MODE != 0;
+  constexpr bool WANT_R = MODE == 2;
+  constexpr int QW = 64 / LPR;
+  constexpr int NRG = kWaves * QW;
+  constexpr int J = LPR * V;
+  constexpr int RPL = R > LPR ? R / LPR : 1;
+  using T = Tile<V, R>;
+
+  __shared__ float s_red[kWaves][J];
+  __shared__ float s_g[J];
+  __shared__ double s_fin[2][kWaves];
+
+  if (a.st->done) return;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane % LPR, q = lane / LPR;
+  const int rg = w * QW + q;
+  const int64_t K = a.K, d = a.d;
+  const int64_t nch = (d + J - 1) / J;
+  const int64_t grid = gridDim.x;
+
+  // Row r of this thread = wave-uniform base (SGPR pair) + 32-bit lane offset.
+  const float* base[R];
+  bool rval[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    base[i] = a.X + (int64_t)(w * QW + NRG * i) * a.ldx;
+    rval[i] = rg + (int64_t)NRG * i < K;
+  }
+  const uint32_t loff = (uint32_t)q * (uint32_t)a.ldx;
+
+  float wt[R];
+  float a_noise = 0.f;
+  if constexpr (!INIT) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) wt[i] = rval[i] ? a.coef[rg + NRG * i] : 0.f;
+    a_noise = a.st->a_noise;
+  }
+
+  auto fetch = [&](int64_t ch, T& t) {
+    const int64_t col = ch * J + (int64_t)c * V;
+    const bool cval = ch < nch && col < d;   // V | d: a lane's group is all-in or all-out
+    const uint32_t off = loff + (uint32_t)col;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (cval && rval[i]) {
+        load_cols<V>(base[i] + off, t.x[i]);
+      } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) t.x[i][v] = 0.f;
+      }
+    }
+    if constexpr (INIT) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) t.g[v] = cval ? a.g_old[col + v] : 0.f;
+    } else {
+      const int64_t gj = ch * J + tid;
+      const bool fin = tid < J && ch < nch && gj < d;
+      t.gold = fin ? a.g_old[gj] : 0.f;
+      t.hn = (fin && a.noise == 2) ? a.hnoise[gj] : 0.f;
+    }
+  };
+
+  double row_acc[RPL], row_acc2[RPL];
+#pragma unroll
+  for (int m = 0; m < RPL; ++m) row_acc[m] = row_acc2[m] = 0.0;
+  double mv_acc = 0.0, gn_acc = 0.0;
+
+  auto process = [&](int64_t ch, T& t) {
+    float gv[V];
+    if constexpr (INIT) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) gv[v] = t.g[v];
+      if (w == 0 && q == 0) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) gn_acc += (double)(gv[v] * gv[v]);
+      }
+    } else {
+      // phase A: weighted column sums over this thread's rows ...
+      float acc[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[v] = 0.f;
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] = fmaf(wt[i], t.x[i][v], acc[v]);
+      // ... over the wave's row groups ...
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1)
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] += __shfl_xor(acc[v], o, 64);
+      if (q == 0) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) s_red[w][c * V + v] = acc[v];
+      }
+      __syncthreads();
+      // ... and over the waves: one finisher thread per column writes g'.
+      if (tid < J) {
+        float sum = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < kWaves; ++ww) sum += s_red[ww][tid];
+        const int64_t gj = ch * J + tid;
+        float gnew = 0.f;
+        if (gj < d) {
+          gnew = sum;
+          if (a.noise == 1) {
+            gnew = fmaf(a_noise, normal1(a.seed, kStreamNoise, a.iter, a.col_off + gj), gnew);
+          } else if (a.noise == 2) {
+            gnew = fmaf(a_noise, t.hn, gnew);
+          }
+          a.g_new[gj] = gnew;
+          const float diff = t.gold - gnew;
+          mv_acc += (double)(diff * diff);
+          gn_acc += (double)(gnew * gnew);
+        }
+        s_g[tid] = gnew;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int v = 0; v < V; ++v) gv[v] = s_g[c * V + v];
+    }
+    // phase B: squared distances of this thread's rows to the (new) iterate.
+    float e[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      float s = 0.f;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const float tt = t.x[i][v] - gv[v];
+        s = fmaf(tt, tt, s);
+      }
+      e[i] = s;
+    }
+    transpose_reduce<LPR, R>(e, c);
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) row_acc[m] += (double)e[m];
+    if constexpr (WANT_R) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        float s = 0.f;
+#pragma unroll
+        for (int v = 0; v < V; ++v) s = fmaf(t.x[i][v], t.x[i][v], s);
+        e[i] = s;
+      }
+      transpose_reduce<LPR, R>(e, c);
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) row_acc2[m] += (double)e[m];
+    }
+  };
+
+  if constexpr (PIPE) {
+    T ta, tb;
+    int64_t ch = blockIdx.x;
+    fetch(ch, ta);
+    for (; ch < nch; ch += 2 * grid) {
+      fetch(ch + grid, tb);
+      process(ch, ta);
+      if (ch + grid >= nch) break;       // block-uniform
+      fetch(ch + 2 * grid, ta);
+      process(ch + grid, tb);
+    }
+  } else {
+    for (int64_t ch = blockIdx.x; ch < nch; ch += grid) {
+      T t;
+      fetch(ch, t);
+      process(ch, t);
+    }
+  }
+
+  // Per-block partials -> slab row.  [D2 (K)] [r (K), INIT only] [mv2] [gn2]
+  double* out = a.slab + (int64_t)blockIdx.x * a.slab_stride;
+  const int i_c = row_of_lane<LPR, R>(c);
+  constexpr int SPAN = R < LPR ? LPR / R : 1;   // lanes holding copies of one row sum
+  if ((c % SPAN) == 0) {
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) {
+      const int64_t k = rg + (int64_t)NRG * (i_c + m);
+      if (k < K) {
+        out[k] = row_acc[m];
+        if constexpr (INIT) out[K + k] = row_acc2[m];
+      }
+    }
+  }
+  const double mv = wave_sum(mv_acc), gn = wave_sum(gn_acc);
+  if (lane == 0) {
+    s_fin[0][w] = mv;
+    s_fin[1][w] = gn;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double m = 0.0, g = 0.0;
+#pragma unroll
+    for (int ww = 0; ww < kWaves; ++ww) {
+      m += s_fin[0][ww];
+      g += s_fin[1][ww];
+    }
+    const int64_t b = INIT ? 2 * K : K;
+    out[b] = m;
+    out[b + 1] = g;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launch plumbing.  GMAGG_PASS_VARIANT: -1 auto (default), 0 plain, 1 pipelined.
+
+static int pass_variant() {
+  static const int v = [] {
+    const char* e = getenv("GMAGG_PASS_VARIANT");
+    return e ? atoi(e) : -1;
+  }();
+  return v;
+}
+
+template <int V, int LPR, int R, int MODE>
+static const void* pass_fn() {
+  // Measured on MI355X (profiles/r01_ab_pass.txt): the plain pass is as fast or
+  // faster at every K; the two-tile variant spills at R*V = 32 and gains
+  // nothing at R*V <= 16, so it is kept for A/B runs only.
+  int pv = pass_variant();
+  if (pv < 0) pv = 0;
+  return pv == 0 ? reinterpret_cast<const void*>(&weiszfeld_pass<V, LPR, R, MODE, false>)
+                 : reinterpret_cast<const void*>(&weiszfeld_pass<V, LPR, R, MODE, true>);
+}
+
+template <int V, int LPR, int R>
+static const void* pass_fn_mode(int mode) {
+  switch (mode) {
+    case 0: return pass_fn<V, LPR, R, 0>();
+    case 1: return pass_fn<V, LPR, R, 1>();
+    default: return pass_fn<V, LPR, R, 2>();
+  }
+}
+
+#define GMK_FOR_EACH_LR(X_, V_)                                                              \
+  X_(V_, 64, 1) X_(V_, 64, 2) X_(V_, 64, 4) X_(V_, 64, 8) X_(V_, 32, 8) X_(V_, 16, 8)         \
+  X_(V_, 8, 8) X_(V_, 4, 8)
+
+static const void* pass_kernel(const PassCfg& cfg, int mode) {
+#define GMK_CASE(V_, L_, R_) \
+  if (cfg.V == V_ && cfg.LPR == L_ && cfg.R == R_) return pass_fn_mode<V_, L_, R_>(mode);
+  GMK_FOR_EACH_LR(GMK_CASE, 4)
+  GMK_FOR_EACH_LR(GMK_CASE, 2)
+  GMK_FOR_EACH_LR(GMK_CASE, 1)
+#undef GMK_CASE
+  return nullptr;
+}
+
+bool pass_cfg_supported(const PassCfg& cfg) { return pass_kernel(cfg, 0) != nullptr; }
+
+hipError_t launch_pass(const PassCfg& cfg, int mode, int grid, const PassArgs& a, hipStream_t s) {
+  const void* fn = pass_kernel(cfg, mode);
+  if (!fn) return hipErrorInvalidValue;
+  void* args[] = {const_cast<PassArgs*>(&a)};
+  return hipLaunchKernel(fn, dim3(grid), dim3(kTPB), args, 0, s);
+}
+
+int pass_blocks_per_cu(const PassCfg& cfg, int mode) {
+  const void* fn = pass_kernel(cfg, mode);
+  int n = 0;
+  if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kTPB, 0) != hipSuccess || n < 1)
+    return 1;
+  return n;
+}
+
+}  // namespace gmk

@@ -1,0 +1,129 @@
+"""d-sharded aggregation through libgmagg's real host loop, on ONE GPU.
+
+P "virtual ranks" run in P threads, each with its own context holding a column
+shard; their all-reduce callback sums the (K+2)-vectors across threads.  The
+sharded result must equal the unsharded one: for gm2 to fp32 reduction order,
+and for AirComp gm with Philox noise too (draws are keyed by global index, so
+shards regenerate the same channel and noise without communicating).  The
+native RCCL path is exercised with a single-rank communicator (one GPU here).
+"""
+import ctypes as C
+import threading
+
+import pytest
+import torch
+
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+
+def _problem(K, d, B, seed):
+    g = torch.Generator().manual_seed(seed)
+    p = 0.07 * torch.randn(d, generator=g)
+    X = p + 5e-4 * torch.randn(K, d, generator=g)
+    X[K - B:] = p + 5e-3 * torch.randn(B, d, generator=g) + 2e-3
+    return X.cuda(), p.cuda()
+
+
+def _sharded(X, p, P, opts, aircomp):
+    from byzantine_aircomp_amd import _lib
+    from byzantine_aircomp_amd.aggregators import Context
+    from byzantine_aircomp_amd.sharded import _wrap, shard_range
+
+    K, d = X.shape
+    dev = X.device
+    barrier = threading.Barrier(P)
+    bufs = [None] * P
+    out = [None] * P
+    errs = []
+
+    def run(r):
+        try:
+            lo, hi = shard_range(d, P, r)
+            ctx = Context(dev.index)
+            ctx.set_shard(d, lo)
+
+            def allreduce(ptr, count, stream):
+                torch.cuda.synchronize(dev)
+                t = _wrap(ptr, count, dev)
+                bufs[r] = t.clone()
+                barrier.wait()
+                total = torch.stack(bufs).sum(0)
+                barrier.wait()
+                t.copy_(total)
+                torch.cuda.synchronize(dev)
+            ctx.set_allreduce(allreduce)
+            Xs = X[:, lo:hi].contiguous()
+            g0 = p[lo:hi].contiguous()
+            res = torch.empty(hi - lo, device=dev)
+            o = _lib.GmOpts()
+            o.maxiter, o.tol, o.eps = opts["maxiter"], opts["tol"], 1e-4
+            o.mode = _lib.GM_MODE_AIRCOMP if aircomp else _lib.GM_MODE_IDEAL
+            if aircomp:
+                o.has_noise, o.noise_var, o.P_max, o.seed = 1, opts["noise_var"], 1.0, opts["seed"]
+            rr = _lib.GmResult()
+            _lib.check(ctx.lib.gm_weiszfeld_f32(ctx.handle, Xs.data_ptr(), K, hi - lo, hi - lo,
+                                                g0.data_ptr(), res.data_ptr(), C.byref(o),
+                                                C.byref(rr), None), "sharded gm")
+            torch.cuda.synchronize(dev)
+            out[r] = (lo, hi, res, rr.iters)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            barrier.abort()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs, errs
+    full = torch.empty(d, device=dev)
+    iters = {o_[3] for o_ in out}
+    for lo, hi, res, _ in out:
+        full[lo:hi] = res
+    return full, iters
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_sharded_gm2_equals_unsharded(P):
+    import byzantine_aircomp_amd as bz
+    X, p = _problem(200, 50_000, 40, seed=P)
+    opts = {"maxiter": 1000, "tol": 1e-5}
+    want = bz.gm2(X, dict(opts, guess=p))
+    n = bz.aggregators.last_result.iters
+    got, iters = _sharded(X, p, P, opts, aircomp=False)
+    assert iters == {n} or max(abs(i - n) for i in iters) <= 1
+    assert len(iters) == 1                          # every shard took the same decisions
+    assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-6
+
+
+def test_sharded_gm_philox_equals_unsharded():
+    import byzantine_aircomp_amd as bz
+    X, p = _problem(50, 7850 * 4, 10, seed=9)
+    opts = {"maxiter": 40, "tol": 1e-5, "noise_var": 1e-2, "seed": 4242}
+    want = bz.gm(X, dict(opts, guess=p))
+    got, iters = _sharded(X, p, 2, opts, aircomp=True)
+    assert iters == {40}
+    assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-5
+
+
+def test_rccl_single_rank_path():
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd import _lib
+    from byzantine_aircomp_amd.aggregators import Context
+    X, p = _problem(64, 10_000, 12, seed=3)
+    want = bz.gm2(X, {"maxiter": 1000, "guess": p})
+    ctx = Context(X.device.index)
+    buf = C.create_string_buffer(128)
+    _lib.check(ctx.lib.gm_rccl_get_unique_id(buf), "uid")
+    ctx.init_rccl(buf.raw, 1, 0)
+    ctx.set_shard(10_000, 0)
+    out = torch.empty(10_000, device="cuda")
+    o = _lib.GmOpts()
+    o.maxiter, o.tol, o.eps = 1000, 1e-5, 1e-4
+    rr = _lib.GmResult()
+    _lib.check(ctx.lib.gm_weiszfeld_f32(ctx.handle, X.data_ptr(), 64, 10_000, 10_000, p.data_ptr(),
+                                        out.data_ptr(), C.byref(o), C.byref(rr), None), "rccl gm2")
+    torch.cuda.synchronize()
+    assert rel_l2(out.cpu().numpy(), want.cpu().numpy()) <= 1e-7
