@@ -63,6 +63,23 @@ def shard_range(d, n, r, align=256):
     return lo, min(d, lo + per)
 
 
+def pmc_traffic(workload):
+    """Per-launch HBM bytes of the STEP pass from the newest committed PMC summary
+    (rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same bench workload;
+    tools/pmc_summary.py applies the gfx950 FETCH_SIZE x2 correction)."""
+    import glob
+    import re
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}.json")))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))
+    for name, row in data["kernels"].items():
+        m = re.search(r"weiszfeld_pass<([^>]*)>", name)
+        if m and m.group(1).split(", ")[-2] == "0":
+            return row["hbm_bytes_per_launch"] / 1e9, os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def cpu_baseline(X, g0, iters, d_full):
     """Time the oracle gm2 (PyTorch CPU, op-for-op the reference) on a sample."""
     from oracle import aggregators as orc
@@ -148,6 +165,7 @@ def main():
         per_launch_bytes = 4.0 * K * d
         avg_pass_s = (pass_ms / 1e3) / max(launches, 1)
         achieved = per_launch_bytes / avg_pass_s / 1e9
+        traffic, traffic_src = pmc_traffic(args.workload) if world == 1 else (None, None)
         line = {
             "metric": "GM aggregations/sec at K=1000,d=11M; % HBM roofline; 1/2/4/8 GPUs",
             "value": args.steps / elapsed,
@@ -168,7 +186,8 @@ def main():
                        "algo": res.algo, "parallelism": f"d-shard x{world}" if world > 1 else "none",
                        "passes_per_aggregation": res.iters + 1},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_unit": "GB per launch", "traffic_source": traffic_src,
                          "kernel": "weiszfeld_pass (STEP)", "launches_timed": launches,
                          "avg_launch_us": avg_pass_s * 1e6,
                          "algorithmic_bytes_per_launch": per_launch_bytes},

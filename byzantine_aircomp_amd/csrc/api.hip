@@ -141,7 +141,7 @@ int allreduce(gm_ctx* c, double* buf, int64_t n, hipStream_t s) {
 // R rows each cover K.  Bigger K -> narrower chunk, so a block's tile (and the
 // bytes it has in flight) stays ~64-128 KiB.
 bool pick_cfg(int64_t K, int V, int64_t ldx, PassCfg* cfg) {
-  int lpr, r;
+  int nw = 16, lpr, r;
   if (K <= 16) { lpr = 64; r = 1; }
   else if (K <= 32) { lpr = 64; r = 2; }
   else if (K <= 64) { lpr = 64; r = 4; }
@@ -151,9 +151,16 @@ bool pick_cfg(int64_t K, int V, int64_t ldx, PassCfg* cfg) {
   else if (K <= 1024) { lpr = 8; r = 8; }
   else if (K <= 2048) { lpr = 4; r = 8; }
   else return false;
+  // GMAGG_PASS_CFG="NW,LPR,R" forces a tile (tuning runs); it must cover K.
+  if (const char* e = getenv("GMAGG_PASS_CFG")) {
+    int a = 0, b = 0, c2 = 0;
+    if (sscanf(e, "%d,%d,%d", &a, &b, &c2) == 3 && (int64_t)a * (64 / b) * c2 >= K) {
+      nw = a; lpr = b; r = c2;
+    }
+  }
   // lane offsets are 32-bit: (rows per wave - 1) * ldx + ldx must fit in bytes
   if ((uint64_t)(64 / lpr) * (uint64_t)ldx * 4u >= (1ull << 32)) return false;
-  *cfg = PassCfg{V, lpr, r};
+  *cfg = PassCfg{V, nw, lpr, r};
   return pass_cfg_supported(*cfg);
 }
 

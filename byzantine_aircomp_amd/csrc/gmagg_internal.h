@@ -20,10 +20,11 @@ struct alignas(64) KState {
   double pad[4];
 };
 
-// Streaming pass configuration: V floats per lane per row, LPR lanes per row
-// segment (chunk width J = LPR*V columns), R rows per thread.
+// Streaming pass configuration: V floats per lane per row, NW waves per
+// block, LPR lanes per row segment (chunk width J = LPR*V columns), R rows
+// per thread (the block covers NW*(64/LPR)*R rows).
 struct PassCfg {
-  int V, LPR, R;
+  int V, NW, LPR, R;
 };
 
 struct PassArgs {

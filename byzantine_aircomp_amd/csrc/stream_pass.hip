@@ -36,19 +36,20 @@ struct Tile {
 
 // MODE: 0 step, 1 init, 2 init + ||x_k||^2.  PIPE: chunk c+1's loads are in
 // flight while chunk c is reduced (two tiles of registers).
-template <int V, int LPR, int R, int MODE, bool PIPE>
-__global__ void __launch_bounds__(kTPB) weiszfeld_pass(PassArgs a) {
+template <int V, int NW, int LPR, int R, int MODE, bool PIPE>
+__global__ void __launch_bounds__(NW * 64) weiszfeld_pass(PassArgs a) {
   constexpr bool INIT = MODE != 0;
   constexpr bool WANT_R = MODE == 2;
   constexpr int QW = 64 / LPR;
-  constexpr int NRG = kWaves * QW;
+  constexpr int NRG = NW * QW;
   constexpr int J = LPR * V;
   constexpr int RPL = R > LPR ? R / LPR : 1;
+  static_assert(J <= NW * 64, "one finisher thread per column");
   using T = Tile<V, R>;
 
-  __shared__ float s_red[kWaves][J];
+  __shared__ float s_red[NW][J];
   __shared__ float s_g[J];
-  __shared__ double s_fin[2][kWaves];
+  __shared__ double s_fin[2][NW];
 
   if (a.st->done) return;
 
@@ -139,7 +140,7 @@ __global__ void __launch_bounds__(kTPB) weiszfeld_pass(PassArgs a) {
       if (tid < J) {
         float sum = 0.f;
 #pragma unroll
-        for (int ww = 0; ww < kWaves; ++ww) sum += s_red[ww][tid];
+        for (int ww = 0; ww < NW; ++ww) sum += s_red[ww][tid];
         const int64_t gj = ch * J + tid;
         float gnew = 0.f;
         if (gj < d) {
@@ -231,7 +232,7 @@ __global__ void __launch_bounds__(kTPB) weiszfeld_pass(PassArgs a) {
   if (tid == 0) {
     double m = 0.0, g = 0.0;
 #pragma unroll
-    for (int ww = 0; ww < kWaves; ++ww) {
+    for (int ww = 0; ww < NW; ++ww) {
       m += s_fin[0][ww];
       g += s_fin[1][ww];
     }
@@ -252,36 +253,41 @@ static int pass_variant() {
   return v;
 }
 
-template <int V, int LPR, int R, int MODE>
+template <int V, int NW, int LPR, int R, int MODE>
 static const void* pass_fn() {
   // Measured on MI355X (profiles/r01_ab_pass.txt): the plain pass is as fast or
   // faster at every K; the two-tile variant spills at R*V = 32 and gains
-  // nothing at R*V <= 16, so it is kept for A/B runs only.
-  int pv = pass_variant();
-  if (pv < 0) pv = 0;
-  return pv == 0 ? reinterpret_cast<const void*>(&weiszfeld_pass<V, LPR, R, MODE, false>)
-                 : reinterpret_cast<const void*>(&weiszfeld_pass<V, LPR, R, MODE, true>);
+  // nothing at R*V <= 16, so it is only built with -DGMK_PIPE_VARIANT for A/B runs.
+#ifdef GMK_PIPE_VARIANT
+  if (pass_variant() == 1)
+    return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, true>);
+#endif
+  return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, false>);
 }
 
-template <int V, int LPR, int R>
+template <int V, int NW, int LPR, int R>
 static const void* pass_fn_mode(int mode) {
   switch (mode) {
-    case 0: return pass_fn<V, LPR, R, 0>();
-    case 1: return pass_fn<V, LPR, R, 1>();
-    default: return pass_fn<V, LPR, R, 2>();
+    case 0: return pass_fn<V, NW, LPR, R, 0>();
+    case 1: return pass_fn<V, NW, LPR, R, 1>();
+    default: return pass_fn<V, NW, LPR, R, 2>();
   }
 }
 
-#define GMK_FOR_EACH_LR(X_, V_)                                                              \
-  X_(V_, 64, 1) X_(V_, 64, 2) X_(V_, 64, 4) X_(V_, 64, 8) X_(V_, 32, 8) X_(V_, 16, 8)         \
-  X_(V_, 8, 8) X_(V_, 4, 8)
+// (waves per block, lanes per row segment, rows per thread) tiles built.
+#define GMK_FOR_EACH_CFG(X_, V_)                                                             \
+  X_(V_, 16, 64, 1) X_(V_, 16, 64, 2) X_(V_, 16, 64, 4) X_(V_, 16, 64, 8) X_(V_, 16, 32, 8)  \
+  X_(V_, 16, 16, 8) X_(V_, 16, 8, 8) X_(V_, 16, 4, 8) X_(V_, 16, 4, 4) X_(V_, 16, 16, 4)     \
+  X_(V_, 8, 8, 16) X_(V_, 8, 4, 8) X_(V_, 8, 16, 8) X_(V_, 8, 8, 8) X_(V_, 4, 8, 8)          \
+  X_(V_, 4, 16, 4) X_(V_, 8, 32, 4)
 
 static const void* pass_kernel(const PassCfg& cfg, int mode) {
-#define GMK_CASE(V_, L_, R_) \
-  if (cfg.V == V_ && cfg.LPR == L_ && cfg.R == R_) return pass_fn_mode<V_, L_, R_>(mode);
-  GMK_FOR_EACH_LR(GMK_CASE, 4)
-  GMK_FOR_EACH_LR(GMK_CASE, 2)
-  GMK_FOR_EACH_LR(GMK_CASE, 1)
+#define GMK_CASE(V_, W_, L_, R_)                                                    \
+  if (cfg.V == V_ && cfg.NW == W_ && cfg.LPR == L_ && cfg.R == R_)                  \
+    return pass_fn_mode<V_, W_, L_, R_>(mode);
+  GMK_FOR_EACH_CFG(GMK_CASE, 4)
+  GMK_FOR_EACH_CFG(GMK_CASE, 2)
+  GMK_FOR_EACH_CFG(GMK_CASE, 1)
 #undef GMK_CASE
   return nullptr;
 }
@@ -292,13 +298,14 @@ hipError_t launch_pass(const PassCfg& cfg, int mode, int grid, const PassArgs& a
   const void* fn = pass_kernel(cfg, mode);
   if (!fn) return hipErrorInvalidValue;
   void* args[] = {const_cast<PassArgs*>(&a)};
-  return hipLaunchKernel(fn, dim3(grid), dim3(kTPB), args, 0, s);
+  return hipLaunchKernel(fn, dim3(grid), dim3(cfg.NW * 64), args, 0, s);
 }
 
 int pass_blocks_per_cu(const PassCfg& cfg, int mode) {
   const void* fn = pass_kernel(cfg, mode);
   int n = 0;
-  if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kTPB, 0) != hipSuccess || n < 1)
+  if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, cfg.NW * 64, 0) != hipSuccess ||
+      n < 1)
     return 1;
   return n;
 }
