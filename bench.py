@@ -50,7 +50,7 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
-    p.add_argument("--algo", default="auto", choices=["auto", "stream", "twopass"])
+    p.add_argument("--algo", default="auto", choices=["auto", "stream", "twopass", "gram"])
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-d", type=int, default=2_000_000, help="CPU sample width")
     return p.parse_args()

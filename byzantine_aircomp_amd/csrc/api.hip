@@ -76,9 +76,15 @@ struct Workspace {
   float* h_re;   // host-noise device copies
   float* h_im;
   float* hnoise; // d local + 1
+  // Gram variant
+  float* gslab;  // [blocks][tiles][1024] fp32 partial Grams
+  double* G;     // [KP][KP]
+  double* alpha;
+  double* u;
 };
 
-int ensure_ws(gm_ctx* c, int64_t K, int64_t d, int nb, Workspace* w) {
+int ensure_ws(gm_ctx* c, int64_t K, int64_t d, int nb, Workspace* w, size_t gram_slab_n = 0,
+              int KP = 0) {
   const int64_t S = 2 * K + 2;
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
@@ -92,6 +98,11 @@ int ensure_ws(gm_ctx* c, int64_t K, int64_t d, int nb, Workspace* w) {
   const size_t o_hr = take(sizeof(float) * K);
   const size_t o_hi = take(sizeof(float) * K);
   const size_t o_hn = take(sizeof(float) * (d + 1));
+  const size_t o_gs = take(sizeof(float) * gram_slab_n);
+  const size_t o_G = take(sizeof(double) * (size_t)KP * KP);
+  const size_t o_al = take(sizeof(double) * K);
+  const size_t o_u = take(sizeof(double) * K);
+  w->gslab = nullptr;
   if (off > c->ws_bytes) {
     if (c->ws) HIPCHK(hipFree(c->ws));
     c->ws = nullptr;
@@ -110,6 +121,10 @@ int ensure_ws(gm_ctx* c, int64_t K, int64_t d, int nb, Workspace* w) {
   w->h_re = reinterpret_cast<float*>(b + o_hr);
   w->h_im = reinterpret_cast<float*>(b + o_hi);
   w->hnoise = reinterpret_cast<float*>(b + o_hn);
+  w->gslab = reinterpret_cast<float*>(b + o_gs);
+  w->G = reinterpret_cast<double*>(b + o_G);
+  w->alpha = reinterpret_cast<double*>(b + o_al);
+  w->u = reinterpret_cast<double*>(b + o_u);
   return GM_OK;
 }
 
@@ -192,6 +207,51 @@ int record_pass_end(gm_ctx* c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   if (!c->timing) return GM_OK;
   HIPCHK(hipEventRecord(e1, s));
   c->ev_used.emplace_back(e0, e1);
+  return GM_OK;
+}
+
+// Gram-space gm2 (gram.hip): G = X'X'^T once (MFMA), the Weiszfeld loop in K-space
+// (one launch, fp64), one closing pass g = sum_k a_k x_k.  Two reads of X.
+int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const float* guess0,
+             float* out, const gm_opts* o, gm_result* res, const PassCfg& cfg, hipStream_t s) {
+  const int KT = gram_kt(K), KP = 32 * KT;
+  const int nb_g = std::max(1, std::min(4 * c->num_cu, (int)((d + 4095) / 4096)));
+  const int J = cfg.LPR * cfg.V;
+  const int nb_p = (int)std::max<int64_t>(
+      1, std::min<int64_t>((d + J - 1) / J, (int64_t)c->num_cu * pass_blocks_per_cu(cfg, 3)));
+  Workspace w;
+  int rc = ensure_ws(c, K, d, 1, &w, gram_slab_floats(KT, nb_g), KP);
+  if (rc) return rc;
+  rc = ensure_host(c, sizeof(KState));
+  if (rc) return rc;
+  KState* hst = reinterpret_cast<KState*>(c->host);
+  HIPCHK(hipMemsetAsync(w.st, 0, sizeof(KState), s));
+  // centre p = guess0, staged to an aligned workspace copy (float4 loads)
+  float* p = w.g[1];
+  HIPCHK(hipMemcpyAsync(p, guess0, sizeof(float) * d, hipMemcpyDeviceToDevice, s));
+  hipEvent_t e0, e1;
+  rc = record_pass_begin(c, s, &e0, &e1);
+  if (rc) return rc;
+  HIPCHK(launch_gram(X, K, d, ldx, p, nb_g, w.gslab, w.G, s));
+  rc = record_pass_end(c, s, e0, e1);
+  if (rc) return rc;
+  rc = allreduce(c, w.G, (int64_t)KP * KP, s);
+  if (rc) return rc;
+  HIPCHK(launch_gram_solve(w.G, KP, K, o->maxiter, (float)o->tol, (float)o->eps, w.alpha, w.u,
+                           w.coef, w.st, s));
+  PassArgs a{};
+  a.X = X; a.K = K; a.d = d; a.ldx = ldx;
+  a.g_old = p; a.g_new = out; a.coef = w.coef; a.st = w.st;
+  a.slab = w.slab; a.slab_stride = 0;
+  HIPCHK(launch_pass(cfg, 3, nb_p, a, s));
+  HIPCHK(hipMemcpyAsync(hst, w.st, sizeof(KState), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  gm_result r{};
+  r.iters = hst->iters;
+  r.last_movement = hst->last_movement;
+  r.converged = hst->converged;
+  r.algo_used = GM_ALGO_GRAM;
+  if (res) *res = r;
   return GM_OK;
 }
 
@@ -323,7 +383,15 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       return fail(GM_ERR_UNSUPPORTED, "streaming pass supports K <= 2048 (K=%lld)", (long long)K);
     else algo = GM_ALGO_TWOPASS;
   }
-  if (algo == GM_ALGO_GRAM) return fail(GM_ERR_UNSUPPORTED, "Gram variant not in this build");
+  if (algo == GM_ALGO_GRAM) {
+    if (o->mode != GM_MODE_IDEAL)
+      return fail(GM_ERR_UNSUPPORTED, "Gram variant is gm2 only (AirComp noise leaves span(X))");
+    if (gram_kt(K) == 0 || V != 4 || !pick_cfg(K, V, ldx, &cfg))
+      return fail(GM_ERR_UNSUPPORTED, "Gram variant needs K <= 256, d and ldx multiples of 4, "
+                  "16-byte aligned X (K=%lld d=%lld ldx=%lld)", (long long)K, (long long)d,
+                  (long long)ldx);
+    return run_gram(c, X, K, d, ldx, guess0, out, o, res, cfg, s);
+  }
   if (algo != GM_ALGO_STREAM && algo != GM_ALGO_TWOPASS)
     return fail(GM_ERR_INVALID, "unknown algo %d", o->algo);
   const int init_mode = o->mode == GM_MODE_AIRCOMP ? 2 : 1;   // ||x_k||^2 only for AirComp

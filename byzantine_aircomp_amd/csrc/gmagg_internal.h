@@ -76,6 +76,15 @@ hipError_t launch_twopass(bool init, const float* X, int64_t K, int64_t d, int64
                           int64_t col_off, double* slab, int nb, double* sums, hipStream_t s);
 int twopass_blocks(int64_t K, int64_t d, int num_cu);
 
+// Gram-space variant (gram.hip).  KT = K padded to 32-row tiles (0: unsupported).
+int gram_kt(int64_t K);
+size_t gram_slab_floats(int KT, int nb);
+hipError_t launch_gram(const float* X, int64_t K, int64_t d, int64_t ldx, const float* p, int nb,
+                       float* slab, double* G, hipStream_t s);
+hipError_t launch_gram_solve(const double* G, int KP, int64_t K, int64_t maxiter, float tol,
+                             float eps, double* alpha, double* u, float* coef, KState* st,
+                             hipStream_t s);
+
 // OMA / synthetic fills (oma.hip).
 hipError_t launch_oma_apply(float* X, int64_t K, int64_t d, int64_t ldx, const float* hr,
                             const float* hi, const float* nr, const float* ni, hipStream_t s);

@@ -38,7 +38,8 @@ struct Tile {
 // flight while chunk c is reduced (two tiles of registers).
 template <int V, int NW, int LPR, int R, int MODE, bool PIPE>
 __global__ void __launch_bounds__(NW * 64) weiszfeld_pass(PassArgs a) {
-  constexpr bool INIT = MODE != 0;
+  constexpr bool SUM_ONLY = MODE == 3;     // closing pass of the Gram variant: g = sum c_k x_k
+  constexpr bool INIT = MODE == 1 || MODE == 2;
   constexpr bool WANT_R = MODE == 2;
   constexpr int QW = 64 / LPR;
   constexpr int NRG = NW * QW;
@@ -51,7 +52,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_pass(PassArgs a) {
   __shared__ float s_g[J];
   __shared__ double s_fin[2][NW];
 
-  if (a.st->done) return;
+  if (!SUM_ONLY && a.st->done) return;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -161,6 +162,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_pass(PassArgs a) {
 #pragma unroll
       for (int v = 0; v < V; ++v) gv[v] = s_g[c * V + v];
     }
+    if constexpr (SUM_ONLY) return;
     // phase B: squared distances of this thread's rows to the (new) iterate.
     float e[R];
 #pragma unroll
@@ -209,6 +211,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_pass(PassArgs a) {
     }
   }
 
+  if constexpr (SUM_ONLY) return;
   // Per-block partials -> slab row.  [D2 (K)] [r (K), INIT only] [mv2] [gn2]
   double* out = a.slab + (int64_t)blockIdx.x * a.slab_stride;
   const int i_c = row_of_lane<LPR, R>(c);
@@ -245,6 +248,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_pass(PassArgs a) {
 // ---------------------------------------------------------------------------
 // Launch plumbing.  GMAGG_PASS_VARIANT: -1 auto (default), 0 plain, 1 pipelined.
 
+#ifdef GMK_PIPE_VARIANT
 static int pass_variant() {
   static const int v = [] {
     const char* e = getenv("GMAGG_PASS_VARIANT");
@@ -252,6 +256,7 @@ static int pass_variant() {
   }();
   return v;
 }
+#endif
 
 template <int V, int NW, int LPR, int R, int MODE>
 static const void* pass_fn() {
@@ -270,7 +275,8 @@ static const void* pass_fn_mode(int mode) {
   switch (mode) {
     case 0: return pass_fn<V, NW, LPR, R, 0>();
     case 1: return pass_fn<V, NW, LPR, R, 1>();
-    default: return pass_fn<V, NW, LPR, R, 2>();
+    case 2: return pass_fn<V, NW, LPR, R, 2>();
+    default: return pass_fn<V, NW, LPR, R, 3>();
   }
 }
 

@@ -208,3 +208,63 @@ def test_gm2_large_fixed_point_property():
     # grad / sum(w) is the next Weiszfeld step g' - g: at convergence its norm is
     # of the order of the tol-test movement
     assert float(grad.norm() / w.sum()) < 1e-4
+
+
+# --- Gram-space variant (north_star's second design) ---------------------------
+
+@pytest.mark.parametrize("name", golden_names("gm2"))
+def test_gram_matches_reference(name):
+    meta, arr = golden_case(name)
+    K, d = arr["X"].shape
+    o = _opts(meta, arr)
+    o["algo"] = "gram"
+    X = torch.from_numpy(arr["X"].copy()).cuda()
+    if meta["options"].get("maxiter", 200) == 0:
+        assert bz().gm2(X, o) is o["guess"]
+        return
+    if d % 4 or K > 256:
+        with pytest.raises(bz()._lib.GmError):
+            bz().gm2(X, o)
+        return
+    out = bz().gm2(X, o)
+    res = bz().aggregators.last_result
+    assert res.algo == "gram"
+    assert rel_l2(out.cpu().numpy(), arr["out"]) <= TOL
+    assert abs(res.iters - meta["iters"]) <= ITER_SLACK
+
+
+@pytest.mark.parametrize("K", [1, 8, 32, 33, 64, 100, 128, 200, 256])
+@pytest.mark.parametrize("d", [4, 4096, 100_000])
+def test_gram_shapes_vs_oracle(K, d):
+    g = torch.Generator().manual_seed(K * 31 + d)
+    p = 0.07 * torch.randn(d, generator=g)
+    X = p + 5e-4 * torch.randn(K, d, generator=g)
+    B = K // 5
+    if B:
+        X[K - B:] += 5e-3 * torch.randn(B, d, generator=g) + 2e-3
+    opts = {"maxiter": 1000, "tol": 1e-5, "guess": p.clone()}
+    want, tr = orc.gm2(X.clone(), dict(opts))
+    got = bz().gm2(X.cuda(), dict(opts, guess=p.cuda(), algo="gram"))
+    assert bz().aggregators.last_result.algo == "gram"
+    assert rel_l2(got.cpu().numpy(), want.numpy()) <= TOL
+    assert abs(bz().aggregators.last_result.iters - tr.iters) <= max(ITER_SLACK, tr.iters // 10)
+
+
+def test_gram_matches_stream_at_c4_scale():
+    """K=256 x d=4M synthetic (C4 recipe): Gram and streaming agree."""
+    m = bz()
+    K, d = 256, 4_000_000
+    X = torch.empty(K, d, device="cuda")
+    ctx = m.context()
+    s = torch.cuda.current_stream().cuda_stream
+    m._lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, X.data_ptr(), K, d, d, 51, 0.0, 0.05,
+                                             0.25, 0.5, 20211, s), "fill")
+    g0 = torch.empty(d, device="cuda")
+    m._lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), d, 0.0, 0.01, 20212, s),
+                 "fill")
+    a = m.gm2(X, {"maxiter": 1000, "guess": g0, "algo": "stream"})
+    na = m.aggregators.last_result.iters
+    b = m.gm2(X, {"maxiter": 1000, "guess": g0, "algo": "gram"})
+    nb = m.aggregators.last_result.iters
+    assert abs(na - nb) <= 1
+    assert rel_l2(b.cpu().numpy(), a.cpu().numpy()) <= TOL
