@@ -1,0 +1,73 @@
+"""Many independent aggregations in one launch per pass (BASELINE C5).
+
+The reference's results figure (draw.ipynb) is a sweep over aggregator x noise
+variance x Byzantine count, each point being thousands of `gm2`/`gm` calls.
+Here P problems [P, K, d] run together: every streaming pass covers all of
+them (grid = chunk blocks x problems), each problem keeps its own K-space
+state and stops at its own tol test (gm2) or runs to maxiter (gm, which never
+meets tol).  AirComp problems draw from Philox, problem p keyed with
+seed + p * 0x9E3779B97F4A7C15, so problem p equals a single `gm` call with that
+seed.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+from .aggregators import GMResult, _ALGO_NAMES, _seed, _stream_ptr, context
+
+__all__ = ["gm2_batched", "gm_batched", "SEED_STRIDE"]
+
+SEED_STRIDE = 0x9E3779B97F4A7C15
+
+
+def _run(X: torch.Tensor, options: dict, aircomp: bool):
+    if X.dim() != 3:
+        raise ValueError(f"X must be [P, K, d] (got {tuple(X.shape)})")
+    if X.device.type != "cuda" or X.dtype != torch.float32:
+        raise TypeError("batched aggregation needs an fp32 CUDA tensor")
+    if X.stride(2) != 1 or X.stride(1) < X.shape[2] or X.stride(0) < X.shape[1] * X.stride(1):
+        X = X.contiguous()
+    P, K, d = X.shape
+    opts = {"maxiter": 200, "tol": 1e-5, "noise_var": None, "P_max": 1}
+    opts.update(options or {})
+    guess = opts.get("guess")
+    if guess is None:
+        guess = X.mean(dim=1)
+    g0 = guess.to(device=X.device, dtype=torch.float32).contiguous()
+    if tuple(g0.shape) != (P, d):
+        raise ValueError(f"guess must be [P, d] = [{P}, {d}]")
+    out = torch.empty(P, d, dtype=torch.float32, device=X.device)
+    o = _lib.GmOpts()
+    o.maxiter = int(opts["maxiter"])
+    o.tol = float(opts["tol"])
+    o.eps = 1e-4
+    o.mode = _lib.GM_MODE_AIRCOMP if aircomp else _lib.GM_MODE_IDEAL
+    o.check_every = int(opts.get("check_every", 0))
+    if aircomp:
+        var = opts["noise_var"]
+        o.has_noise = int(var is not None)
+        o.noise_var = float(var) if var is not None else 0.0
+        o.P_max = float(opts["P_max"])
+        o.seed = _seed(opts)
+    res = (_lib.GmResult * P)()
+    ctx = context(X.device)
+    with torch.cuda.device(X.device):
+        _lib.check(ctx.lib.gm_weiszfeld_batched_f32(
+            ctx.handle, X.data_ptr(), P, K, d, X.stride(1), X.stride(0), g0.data_ptr(), d,
+            out.data_ptr(), d, C.byref(o), res, _stream_ptr(X.device)), "gm_weiszfeld_batched_f32")
+    results = [GMResult(r.iters, r.last_movement, bool(r.converged),
+                        _ALGO_NAMES.get(r.algo_used, "?")) for r in res]
+    return out, results
+
+
+def gm2_batched(X, options=None):
+    """gm2 (M:162-184) on each of P problems X[p] ([P, K, d]) -> ([P, d], results)."""
+    return _run(X, options or {}, aircomp=False)
+
+
+def gm_batched(X, options=None):
+    """AirComp gm (M:131-160) on each of P problems, Philox noise -> ([P, d], results)."""
+    return _run(X, options or {}, aircomp=True)

@@ -540,6 +540,140 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   return GM_OK;
 }
 
+int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_t d,
+                             int64_t ldx, int64_t ldp, const float* guess0, int64_t ldg,
+                             float* out, int64_t ldo, const gm_opts* o, gm_result* results,
+                             void* stream) {
+  if (!c || !o || !X || !guess0 || !out)
+    return fail(GM_ERR_INVALID, "gm_weiszfeld_batched_f32: NULL argument");
+  if (P < 1 || P > 65535 || K < 1 || d < 1 || ldx < d || ldp < K * ldx || ldg < d || ldo < d ||
+      o->maxiter < 0)
+    return fail(GM_ERR_INVALID, "gm_weiszfeld_batched_f32: bad shape P=%lld K=%lld d=%lld",
+                (long long)P, (long long)K, (long long)d);
+  if (o->mode == GM_MODE_AIRCOMP && o->noise_source != GM_NOISE_PHILOX)
+    return fail(GM_ERR_UNSUPPORTED, "batched AirComp uses Philox noise only");
+  if (c->d_total > 0) return fail(GM_ERR_UNSUPPORTED, "batched problems are not d-sharded");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (o->maxiter == 0) {
+    HIPCHK(hipMemcpy2DAsync(out, ldo * 4, guess0, ldg * 4, d * 4, P, hipMemcpyDeviceToDevice, s));
+    if (results)
+      for (int64_t p = 0; p < P; ++p) results[p] = gm_result{0, NAN, 0, GM_ALGO_STREAM};
+    return GM_OK;
+  }
+  PassCfg cfg{};
+  int V = pick_vec(X, d, ldx);
+  if (ldp % V) V = 1;
+  if (!pick_cfg(K, V, ldx, &cfg))
+    return fail(GM_ERR_UNSUPPORTED, "batched streaming pass supports K <= 2048");
+  const int init_mode = o->mode == GM_MODE_AIRCOMP ? 2 : 1;
+  const int J = cfg.LPR * cfg.V;
+  const int64_t nch = (d + J - 1) / J;
+  const int64_t target = (int64_t)c->num_cu * pass_blocks_per_cu(cfg, 0) * 2;
+  const int nbp = (int)std::max<int64_t>(1, std::min<int64_t>(nch, (target + P - 1) / P));
+  const int64_t S = 2 * K + 2;
+
+  // workspace: per problem KState, sums, r, coef, slab[nbp][S], g[2][d]; + a done counter
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t r0 = off; off = align_up(off + bytes, 256); return r0; };
+  const size_t o_st = take(sizeof(KState) * P), o_cnt = take(sizeof(int) * 4);
+  const size_t o_sums = take(sizeof(double) * S * P), o_r = take(sizeof(double) * K * P);
+  const size_t o_coef = take(sizeof(float) * K * P), o_slab = take(sizeof(double) * S * nbp * P);
+  const size_t o_g0 = take(sizeof(float) * d * P), o_g1 = take(sizeof(float) * d * P);
+  if (off > c->ws_bytes) {
+    if (c->ws) HIPCHK(hipFree(c->ws));
+    c->ws = nullptr;
+    c->ws_bytes = 0;
+    HIPCHK(hipMalloc(&c->ws, off));
+    c->ws_bytes = off;
+  }
+  char* b = c->ws;
+  KState* st = reinterpret_cast<KState*>(b + o_st);
+  int* cnt = reinterpret_cast<int*>(b + o_cnt);
+  double* sums = reinterpret_cast<double*>(b + o_sums);
+  double* rr = reinterpret_cast<double*>(b + o_r);
+  float* coef = reinterpret_cast<float*>(b + o_coef);
+  double* slab = reinterpret_cast<double*>(b + o_slab);
+  float* g[2] = {reinterpret_cast<float*>(b + o_g0), reinterpret_cast<float*>(b + o_g1)};
+  int rc = ensure_host(c, sizeof(KState) * P + 256);
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(b, 0, o_sums, s));          // KStates + counter
+
+  KspaceArgs ka{};
+  ka.K = K;
+  ka.d_total = d;
+  ka.mode = o->mode;
+  ka.has_noise = o->mode == GM_MODE_AIRCOMP && o->has_noise;
+  ka.noise_src = 0;
+  ka.tol = (float)o->tol;
+  ka.eps = (float)o->eps;
+  ka.P_max = o->P_max;
+  ka.noise_sd = std::sqrt(std::max(0.0, o->noise_var) / 2.0);
+  ka.seed = o->seed;
+  ka.sums = sums;
+  ka.r = rr;
+  ka.coef = coef;
+  ka.st = st;
+  ka.sums_ps = S;
+  ka.n_done = cnt;
+  const int noise_kind = ka.has_noise ? 1 : 0;
+
+  auto do_pass = [&](int64_t t) -> int {
+    const bool init = t < 0;
+    PassArgs a{};
+    a.X = X; a.K = K; a.d = d; a.ldx = ldx; a.x_ps = ldp;
+    if (init || t == 0) { a.g_old = guess0; a.gold_ps = ldg; }
+    else { a.g_old = g[(t - 1) & 1]; a.gold_ps = d; }
+    a.g_new = init ? nullptr : g[t & 1];
+    a.gnew_ps = d;
+    a.coef = coef; a.st = st; a.slab = slab; a.slab_stride = init ? S : K + 2;
+    a.noise = noise_kind; a.seed = o->seed; a.iter = t;
+    hipEvent_t e0, e1;
+    int rc2 = init ? GM_OK : record_pass_begin(c, s, &e0, &e1);
+    if (rc2) return rc2;
+    HIPCHK(launch_pass(cfg, init ? init_mode : 0, nbp, a, s, (int)P));
+    if (!init) { rc2 = record_pass_end(c, s, e0, e1); if (rc2) return rc2; }
+    HIPCHK(launch_slab_reduce(slab, nbp, init ? S : K + 2, sums, st, s, (int)P, S));
+    return GM_OK;
+  };
+  int* hcnt = reinterpret_cast<int*>(c->host);
+  auto poll_done = [&]() -> int {
+    HIPCHK(hipMemcpyAsync(hcnt, cnt, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return *hcnt;
+  };
+
+  rc = do_pass(-1);
+  if (rc) return rc;
+  ka.t = -1;
+  ka.do_check = 0;
+  ka.do_coef = 1;
+  HIPCHK(launch_kspace(ka, s, (int)P));
+  int check_every = o->check_every > 0 ? o->check_every : 16;
+  for (int64_t t = 0; t < o->maxiter; ++t) {
+    rc = do_pass(t);
+    if (rc) return rc;
+    const bool last = t + 1 == o->maxiter;
+    ka.t = t;
+    ka.do_check = 1;
+    ka.do_coef = last ? 0 : 1;
+    HIPCHK(launch_kspace(ka, s, (int)P));
+    if (!last && (t + 1) % check_every == 0) {
+      const int nd = poll_done();
+      if (nd < 0) return nd;
+      if (nd >= P) break;
+    }
+  }
+  HIPCHK(launch_batched_finalize(g[0], g[1], d, (int)P, st, out, ldo, s));
+  KState* hst = reinterpret_cast<KState*>(c->host);
+  HIPCHK(hipMemcpyAsync(hst, st, sizeof(KState) * P, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (results)
+    for (int64_t p = 0; p < P; ++p)
+      results[p] = gm_result{hst[p].iters, hst[p].last_movement, hst[p].converged, GM_ALGO_STREAM};
+  return GM_OK;
+}
+
 int gm_oma_philox_f32(gm_ctx* c, float* X, int64_t K, int64_t d, int64_t ldx, double noise_var,
                       uint64_t seed, void* stream) {
   if (!c || !X || K < 0 || d < 0 || ldx < d || noise_var < 0)

@@ -42,7 +42,13 @@ struct PassArgs {
   uint64_t seed;
   int64_t iter;           // Weiszfeld iteration index the pass computes
   int64_t col_off;        // global index of local column 0 (d-sharding)
+  // Batched independent problems (BASELINE C5): blockIdx.y = problem p; X,
+  // g_old, g_new advance by these element strides, coef by K, st by 1, slab by
+  // gridDim.x * slab_stride, the Philox seed by p * kSeedStride.  0 / unused for P = 1.
+  int64_t x_ps, gold_ps, gnew_ps;
 };
+
+constexpr uint64_t kSeedStride = 0x9E3779B97F4A7C15ull;
 
 struct KspaceArgs {
   int64_t K, d_total, t;  // t = pass just completed, -1 after the initial pass
@@ -59,22 +65,29 @@ struct KspaceArgs {
   const float* n_last;    // the denominator's noise element
   float* coef;
   KState* st;
+  // Batched: blockIdx.x = problem; sums advance by sums_ps, r / coef by K, st by 1.
+  int64_t sums_ps;
+  int* n_done;            // problems whose tol test has fired (nullable)
 };
 
 // Streaming pass (stream_pass.hip).  mode: 0 step, 1 init, 2 init + ||x_k||^2.
-hipError_t launch_pass(const PassCfg& cfg, int mode, int grid, const PassArgs& a, hipStream_t s);
+hipError_t launch_pass(const PassCfg& cfg, int mode, int grid, const PassArgs& a, hipStream_t s,
+                       int problems = 1);
 int pass_blocks_per_cu(const PassCfg& cfg, int mode);
 bool pass_cfg_supported(const PassCfg& cfg);
 
 // Reduction, K-space step and the two-pass path (weiszfeld.hip).
 hipError_t launch_slab_reduce(const double* slab, int nb, int64_t S, double* sums,
-                              const KState* st, hipStream_t s);
-hipError_t launch_kspace(const KspaceArgs& a, hipStream_t s);
+                              const KState* st, hipStream_t s, int problems = 1,
+                              int64_t sums_ps = 0);
+hipError_t launch_kspace(const KspaceArgs& a, hipStream_t s, int problems = 1);
 hipError_t launch_twopass(bool init, const float* X, int64_t K, int64_t d, int64_t ldx,
                           const float* g_old, float* g_new, const float* coef, const KState* st,
                           int noise, const float* hnoise, uint64_t seed, int64_t iter,
                           int64_t col_off, double* slab, int nb, double* sums, hipStream_t s);
 int twopass_blocks(int64_t K, int64_t d, int num_cu);
+hipError_t launch_batched_finalize(const float* g0, const float* g1, int64_t d, int problems,
+                                   const KState* st, float* out, int64_t ldo, hipStream_t s);
 
 // Gram-space variant (gram.hip).  KT = K padded to 32-row tiles (0: unsupported).
 int gram_kt(int64_t K);

@@ -52,6 +52,16 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_pass(PassArgs a) {
   __shared__ float s_g[J];
   __shared__ double s_fin[2][NW];
 
+  if (gridDim.y > 1) {                       // batched independent problems
+    const int64_t pb = blockIdx.y;
+    a.X += pb * a.x_ps;
+    a.g_old += pb * a.gold_ps;
+    if (a.g_new) a.g_new += pb * a.gnew_ps;
+    a.coef += pb * a.K;
+    a.st += pb;
+    a.slab += pb * (int64_t)gridDim.x * a.slab_stride;
+    a.seed += (uint64_t)pb * kSeedStride;
+  }
   if (!SUM_ONLY && a.st->done) return;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -300,11 +310,12 @@ static const void* pass_kernel(const PassCfg& cfg, int mode) {
 
 bool pass_cfg_supported(const PassCfg& cfg) { return pass_kernel(cfg, 0) != nullptr; }
 
-hipError_t launch_pass(const PassCfg& cfg, int mode, int grid, const PassArgs& a, hipStream_t s) {
+hipError_t launch_pass(const PassCfg& cfg, int mode, int grid, const PassArgs& a, hipStream_t s,
+                       int problems) {
   const void* fn = pass_kernel(cfg, mode);
   if (!fn) return hipErrorInvalidValue;
   void* args[] = {const_cast<PassArgs*>(&a)};
-  return hipLaunchKernel(fn, dim3(grid), dim3(cfg.NW * 64), args, 0, s);
+  return hipLaunchKernel(fn, dim3(grid, problems), dim3(cfg.NW * 64), args, 0, s);
 }
 
 int pass_blocks_per_cu(const PassCfg& cfg, int mode) {

@@ -18,7 +18,11 @@ namespace gmk {
 // Sum the per-block slab rows, column by column, in a fixed order.
 __global__ void __launch_bounds__(1024) slab_reduce(const double* __restrict__ slab, int nb,
                                                     int64_t S, double* __restrict__ sums,
-                                                    const KState* st) {
+                                                    const KState* st, int64_t sums_ps) {
+  const int64_t pb = blockIdx.y;             // batched problems
+  st += pb;
+  slab += pb * nb * S;
+  sums += pb * sums_ps;
   if (st->done) return;
   __shared__ double red[32][33];
   const int cx = threadIdx.x & 31, by = threadIdx.x >> 5;
@@ -39,6 +43,14 @@ __global__ void __launch_bounds__(1024) slab_reduce(const double* __restrict__ s
 // The K-space step: the tol test of the pass that just finished, then the
 // next pass's coefficients.  One block.
 __global__ void __launch_bounds__(1024) kspace_step(KspaceArgs a) {
+  if (gridDim.x > 1) {                       // batched problems: block = problem
+    const int64_t pb = blockIdx.x;
+    a.sums += pb * a.sums_ps;
+    a.r += pb * a.K;
+    a.coef += pb * a.K;
+    a.st += pb;
+    a.seed += (uint64_t)pb * kSeedStride;
+  }
   KState* st = a.st;
   if (st->done) return;
   __shared__ double scratch[16];
@@ -59,6 +71,7 @@ __global__ void __launch_bounds__(1024) kspace_step(KspaceArgs a) {
         st->done = 1;
         st->converged = 1;
         s_stop = 1;
+        if (a.n_done) atomicAdd(a.n_done, 1);
       }
     }
   }
@@ -194,18 +207,41 @@ __global__ void __launch_bounds__(256) twopass_dist(const float* __restrict__ X,
   }
 }
 
+// Batched problems: out_p = the buffer holding problem p's last iterate.
+__global__ void __launch_bounds__(256) batched_finalize(const float* __restrict__ g0,
+                                                        const float* __restrict__ g1, int64_t d,
+                                                        const KState* st, float* out,
+                                                        int64_t ldo) {
+  const int64_t pb = blockIdx.y;
+  const int64_t it = st[pb].iters;
+  const float* src = ((it - 1) & 1) ? g1 : g0;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d;
+       j += (int64_t)gridDim.x * blockDim.x)
+    out[pb * ldo + j] = src[pb * d + j];
+}
+
+hipError_t launch_batched_finalize(const float* g0, const float* g1, int64_t d, int problems,
+                                   const KState* st, float* out, int64_t ldo, hipStream_t s) {
+  const int64_t bx = (d + 255) / 256;
+  hipLaunchKernelGGL(batched_finalize, dim3((unsigned)(bx < 64 ? bx : 64), problems), dim3(256), 0,
+                     s, g0, g1, d, st, out, ldo);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // Launch plumbing.
 
 hipError_t launch_slab_reduce(const double* slab, int nb, int64_t S, double* sums,
-                              const KState* st, hipStream_t s) {
+                              const KState* st, hipStream_t s, int problems, int64_t sums_ps) {
   const int grid = (int)((S + 31) / 32);
-  hipLaunchKernelGGL(slab_reduce, dim3(grid), dim3(1024), 0, s, slab, nb, S, sums, st);
+  hipLaunchKernelGGL(slab_reduce, dim3(grid, problems), dim3(1024), 0, s, slab, nb, S, sums, st,
+                     sums_ps);
   return hipGetLastError();
 }
 
-hipError_t launch_kspace(const KspaceArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(kspace_step, dim3(1), dim3(1024), 0, s, a);
+hipError_t launch_kspace(const KspaceArgs& a, hipStream_t s, int problems) {
+  const int threads = a.K >= 1024 ? 1024 : (int)((a.K + 63) / 64 * 64);
+  hipLaunchKernelGGL(kspace_step, dim3(problems), dim3(threads), 0, s, a);
   return hipGetLastError();
 }
 

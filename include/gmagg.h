@@ -120,6 +120,18 @@ int gm_weiszfeld_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t 
                      const float* guess0, float* out, const gm_opts* opts,
                      gm_result* result, void* stream);
 
+/* Batched independent problems (BASELINE config C5, the draw.ipynb-style sweep
+ * over many small aggregations): problem p aggregates the K rows at X + p*ldp
+ * (row stride ldx) from guess0 + p*ldg into out + p*ldo.  One launch per pass
+ * covers all P problems; each stops at its own tol test (gm2) or runs maxiter
+ * (gm).  Options are shared; GM_MODE_AIRCOMP uses Philox only, problem p keyed
+ * with seed + p * 0x9E3779B97F4A7C15.  results: P entries or NULL.  Not
+ * combinable with d-sharding. */
+int gm_weiszfeld_batched_f32(gm_ctx* ctx, const float* X, int64_t P, int64_t K, int64_t d,
+                             int64_t ldx, int64_t ldp, const float* guess0, int64_t ldg,
+                             float* out, int64_t ldo, const gm_opts* opts, gm_result* results,
+                             void* stream);
+
 /* OMA(message, noise_var): in-place per-client equalised AWGN
  * (MNIST_Air_weight.py:385-394), draws from on-device Philox keyed by `seed`. */
 int gm_oma_philox_f32(gm_ctx* ctx, float* X, int64_t K, int64_t d, int64_t ldx,

@@ -1,0 +1,58 @@
+"""Batched independent aggregations (row f1, BASELINE C5) vs single calls and the oracle."""
+import pytest
+import torch
+
+from conftest import rel_l2
+from oracle import aggregators as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _problems(P, K, d, seed):
+    g = torch.Generator().manual_seed(seed)
+    p = 0.07 * torch.randn(P, 1, d, generator=g)
+    X = p + 5e-4 * torch.randn(P, K, d, generator=g)
+    for i in range(P):
+        B = (0, 5, 10)[i % 3] if K >= 20 else 0
+        if B:
+            X[i, K - B:] = p[i] + 5e-3 * torch.randn(B, d, generator=g) + 2e-3
+    return X, p[:, 0, :]
+
+
+@pytest.mark.parametrize("P,K,d", [(1, 50, 7852), (7, 50, 10_000), (12, 17, 333), (33, 64, 4096)])
+def test_gm2_batched_matches_oracle(P, K, d):
+    from byzantine_aircomp_amd.batched import gm2_batched
+    X, p = _problems(P, K, d, seed=P * 100 + K)
+    out, res = gm2_batched(X.cuda(), {"maxiter": 1000, "guess": p.cuda()})
+    for i in range(P):
+        want, tr = orc.gm2(X[i].clone(), {"maxiter": 1000, "tol": 1e-5, "guess": p[i].clone()})
+        assert rel_l2(out[i].cpu().numpy(), want.numpy()) <= 1e-5
+        assert abs(res[i].iters - tr.iters) <= 1
+
+
+def test_gm_batched_equals_single_calls():
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd.batched import SEED_STRIDE, gm_batched
+    P, K, d = 6, 50, 20_000
+    X, p = _problems(P, K, d, seed=5)
+    X, p = X.cuda(), p.cuda()
+    opts = {"maxiter": 30, "tol": 1e-5, "noise_var": 1e-2, "seed": 99}
+    out, res = gm_batched(X, dict(opts, guess=p))
+    for i in range(P):
+        single = bz.gm(X[i], dict(opts, guess=p[i], seed=(99 + i * SEED_STRIDE) % 2 ** 64))
+        assert rel_l2(out[i].cpu().numpy(), single.cpu().numpy()) <= 1e-6
+        assert res[i].iters == 30
+
+
+def test_batched_mixed_convergence():
+    """Problems converge at different iterations; each stops at its own tol test."""
+    from byzantine_aircomp_amd.batched import gm2_batched
+    X, p = _problems(5, 30, 2048, seed=8)
+    X[2] = torch.randn(30, 2048)            # a harder problem: converges later
+    out, res = gm2_batched(X.cuda(), {"maxiter": 1000, "guess": p.cuda(), "tol": 1e-6})
+    iters = [r.iters for r in res]
+    assert len(set(iters)) > 1
+    for i in range(5):
+        want, tr = orc.gm2(X[i].clone(), {"maxiter": 1000, "tol": 1e-6, "guess": p[i].clone()})
+        assert rel_l2(out[i].cpu().numpy(), want.numpy()) <= 1e-5
+        assert abs(iters[i] - tr.iters) <= 1
