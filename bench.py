@@ -41,7 +41,9 @@ WORKLOADS = {
     "c3-small": (1000, 1_000_000, 200),
     "c4-shard": (256, 15_625_000, 51),     # one GPU's shard of K=256 x d=125M
     "c5-problem": (50, 100_000, 10),
+    "c2": (50, 7850, 10),                   # MNIST MLP d, K=50, B=10 (use --agg gm --var 1e-2)
 }
+MFMA_F32_PEAK_TFLOPS = 157.3                 # v_mfma_f32_32x32x2_f32, dense (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -51,6 +53,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     p.add_argument("--algo", default="auto", choices=["auto", "stream", "twopass", "gram"])
+    p.add_argument("--agg", default="gm2", choices=["gm2", "gm"])
+    p.add_argument("--var", type=float, default=None, help="gm noise variance (None = no AWGN)")
+    p.add_argument("--maxiter", type=int, default=1000)
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-d", type=int, default=2_000_000, help="CPU sample width")
     return p.parse_args()
@@ -134,10 +139,13 @@ def main():
     g0 = torch.empty(d, dtype=torch.float32, device=dev)
     _lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), d, 0.0, 0.01, 20212, stream),
                "fill")
-    opts = {"maxiter": 1000, "tol": 1e-5, "guess": g0, "algo": args.algo}
+    opts = {"maxiter": args.maxiter, "tol": 1e-5, "guess": g0, "algo": args.algo}
+    if args.agg == "gm":
+        opts.update(noise_var=args.var, seed=2021)
+    agg = bz.gm2 if args.agg == "gm2" else bz.gm
 
     def step():
-        return bz.gm2(X, opts)
+        return agg(X, opts)
 
     for _ in range(args.warmup):
         step()
@@ -166,6 +174,25 @@ def main():
         avg_pass_s = (pass_ms / 1e3) / max(launches, 1)
         achieved = per_launch_bytes / avg_pass_s / 1e9
         traffic, traffic_src = pmc_traffic(args.workload) if world == 1 else (None, None)
+        if res.algo == "gram":
+            # dominant kernel = gram_partial: MFMA-bound; FLOPs issued = upper-triangle
+            # 32x32 tiles of the K-padded Gram, 2 FLOP per MAC, d_local columns
+            kt = 1 if K <= 32 else 2 if K <= 64 else 4 if K <= 128 else 8
+            flops = kt * (kt + 1) / 2 * 1024 * 2.0 * d
+            tf = flops / avg_pass_s / 1e12
+            roof = {"bound": "mfma", "achieved": tf, "peak": MFMA_F32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": tf / MFMA_F32_PEAK_TFLOPS, "traffic": None,
+                    "kernel": "gram_partial (v_mfma_f32_32x32x2_f32, upper-triangle tiles)",
+                    "launches_timed": launches, "avg_launch_us": avg_pass_s * 1e6,
+                    "algorithmic_flops_per_launch": flops,
+                    "syrk_flops_per_launch (2*K^2*d)": 2.0 * K * K * d}
+        else:
+            roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                    "traffic_unit": "GB per launch", "traffic_source": traffic_src,
+                    "kernel": "weiszfeld_pass (STEP)", "launches_timed": launches,
+                    "avg_launch_us": avg_pass_s * 1e6,
+                    "algorithmic_bytes_per_launch": per_launch_bytes}
         line = {
             "metric": "GM aggregations/sec at K=1000,d=11M; % HBM roofline; 1/2/4/8 GPUs",
             "value": args.steps / elapsed,
@@ -180,20 +207,16 @@ def main():
             "dtype": "f32",
             "data": "synthetic (Philox on device: honest N(0,0.05^2), last 20% N(0.25,0.5^2), "
                     "guess N(0,0.01^2))",
-            "config": {"workload": f"{args.workload}: gm2 K={K} x d={d_total} fp32, B={B} "
-                                   f"Byzantine, tol 1e-5, maxiter 1000",
+            "config": {"workload": f"{args.workload}: {args.agg} K={K} x d={d_total} fp32, B={B} "
+                                   f"Byzantine, tol 1e-5, maxiter {args.maxiter}"
+                                   + (f", noise_var {args.var}" if args.agg == "gm" else ""),
                        "K": K, "d": d_total, "byzantine": B, "iters": res.iters,
                        "algo": res.algo, "parallelism": f"d-shard x{world}" if world > 1 else "none",
-                       "passes_per_aggregation": res.iters + 1},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_unit": "GB per launch", "traffic_source": traffic_src,
-                         "kernel": "weiszfeld_pass (STEP)", "launches_timed": launches,
-                         "avg_launch_us": avg_pass_s * 1e6,
-                         "algorithmic_bytes_per_launch": per_launch_bytes},
+                       "passes_per_aggregation": res.iters + 1 if res.algo != "gram" else 2},
+            "roofline": roof,
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu:
+        if world == 1 and not args.no_cpu and args.agg == "gm2":
             dc = min(args.cpu_d, d)
             line["cpu_baseline"] = cpu_baseline(X[:, :dc].contiguous(), g0[:dc], res.iters, d_total)
         print(json.dumps(line), flush=True)

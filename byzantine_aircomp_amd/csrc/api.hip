@@ -377,6 +377,12 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   PassCfg cfg{};
   int algo = o->algo;
   const int V = pick_vec(X, d, ldx);
+  // AUTO: Gram-space for gm2 at K <= 256 on large d (MI355X, profiles/r01_cmp_algos.txt:
+  // K=256 x d=15.6M 69.1 vs 56.0 aggregations/s; X read twice instead of n+1 times),
+  // streaming otherwise.
+  if (algo == GM_ALGO_AUTO && o->mode == GM_MODE_IDEAL && gram_kt(K) > 0 && V == 4 &&
+      d >= (int64_t)1 << 18 && pick_cfg(K, V, ldx, &cfg))
+    algo = GM_ALGO_GRAM;
   if (algo == GM_ALGO_AUTO || algo == GM_ALGO_STREAM) {
     if (pick_cfg(K, V, ldx, &cfg)) algo = GM_ALGO_STREAM;
     else if (algo == GM_ALGO_STREAM)
