@@ -54,7 +54,8 @@ class GMResult:
 
 last_result: GMResult | None = None
 _ALGOS = {"auto": _lib.GM_ALGO_AUTO, "stream": _lib.GM_ALGO_STREAM,
-          "twopass": _lib.GM_ALGO_TWOPASS, "gram": _lib.GM_ALGO_GRAM}
+          "twopass": _lib.GM_ALGO_TWOPASS, "gram": _lib.GM_ALGO_GRAM,
+          "resident": _lib.GM_ALGO_RESIDENT}
 _ALGO_NAMES = {v: k for k, v in _ALGOS.items()}
 
 

@@ -210,6 +210,48 @@ int record_pass_end(gm_ctx* c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   return GM_OK;
 }
 
+// Small problems (resident.hip): one cooperative launch, X in VGPRs, every
+// iteration on the device.
+int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
+                 const float* guess0, float* out, const gm_opts* o, gm_result* res,
+                 const PassCfg& cfg, int nch, hipStream_t s) {
+  const int64_t S = 2 * K + 2;
+  Workspace w;
+  int rc = ensure_ws(c, K, d, (int)(2 * nch), &w);   // slab [2][nch][2K+2]
+  if (rc) return rc;
+  rc = ensure_host(c, sizeof(KState));
+  if (rc) return rc;
+  unsigned* bar = reinterpret_cast<unsigned*>(w.sums);  // reuse: 3 words, zeroed per call
+  HIPCHK(hipMemsetAsync(w.st, 0, sizeof(KState), s));
+  HIPCHK(hipMemsetAsync(bar, 0, 16, s));
+  ResArgs a{};
+  a.X = X; a.K = K; a.d = d; a.ldx = ldx; a.guess0 = guess0; a.out = out;
+  a.maxiter = o->maxiter; a.tol = (float)o->tol; a.eps = (float)o->eps;
+  a.mode = o->mode; a.has_noise = o->mode == GM_MODE_AIRCOMP && o->has_noise;
+  a.P_max = o->P_max; a.noise_sd = std::sqrt(std::max(0.0, o->noise_var) / 2.0);
+  a.seed = o->seed; a.slab = w.slab; a.bar = bar; a.st = w.st;
+  (void)S;
+  hipEvent_t e0, e1;
+  rc = record_pass_begin(c, s, &e0, &e1);
+  if (rc) return rc;
+  HIPCHK(launch_resident(cfg, nch, a, s));
+  rc = record_pass_end(c, s, e0, e1);
+  if (rc) return rc;
+  KState* hst = reinterpret_cast<KState*>(c->host);
+  HIPCHK(hipMemcpyAsync(hst, w.st, sizeof(KState), hipMemcpyDeviceToHost, s));
+  unsigned hbar[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpyAsync(hbar, bar, 16, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (hbar[2]) return fail(GM_ERR_HIP, "resident kernel: grid barrier timed out");
+  gm_result r{};
+  r.iters = hst->iters;
+  r.last_movement = hst->last_movement;
+  r.converged = hst->converged;
+  r.algo_used = GM_ALGO_RESIDENT;
+  if (res) *res = r;
+  return GM_OK;
+}
+
 // Gram-space gm2 (gram.hip): G = X'X'^T once (MFMA), the Weiszfeld loop in K-space
 // (one launch, fp64), one closing pass g = sum_k a_k x_k.  Two reads of X.
 int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const float* guess0,
@@ -383,6 +425,18 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   if (algo == GM_ALGO_AUTO && o->mode == GM_MODE_IDEAL && gram_kt(K) > 0 && V == 4 &&
       d >= (int64_t)1 << 18 && pick_cfg(K, V, ldx, &cfg))
     algo = GM_ALGO_GRAM;
+  // Small problems: the register-resident single launch when every chunk fits one
+  // co-resident block (unsharded, Philox or no noise).
+  const bool host_noise_req = o->mode == GM_MODE_AIRCOMP && o->noise_source == GM_NOISE_HOST;
+  if ((algo == GM_ALGO_AUTO || algo == GM_ALGO_RESIDENT) && !host_noise_req &&
+      c->d_total <= 0 && !c->comm && !c->ar_fn && pick_cfg(K, V, ldx, &cfg)) {
+    const int J = cfg.LPR * cfg.V;
+    const int64_t nch = (d + J - 1) / J;
+    if (nch <= resident_max_blocks(cfg, c->num_cu))
+      return run_resident(c, X, K, d, ldx, guess0, out, o, res, cfg, (int)nch, s);
+  }
+  if (algo == GM_ALGO_RESIDENT)
+    return fail(GM_ERR_UNSUPPORTED, "resident kernel: problem too large, sharded or host noise");
   if (algo == GM_ALGO_AUTO || algo == GM_ALGO_STREAM) {
     if (pick_cfg(K, V, ldx, &cfg)) algo = GM_ALGO_STREAM;
     else if (algo == GM_ALGO_STREAM)

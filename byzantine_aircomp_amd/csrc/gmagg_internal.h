@@ -89,6 +89,24 @@ int twopass_blocks(int64_t K, int64_t d, int num_cu);
 hipError_t launch_batched_finalize(const float* g0, const float* g1, int64_t d, int problems,
                                    const KState* st, float* out, int64_t ldo, hipStream_t s);
 
+// Register-resident persistent kernel for small problems (resident.hip).
+struct ResArgs {
+  const float* X;
+  int64_t K, d, ldx;
+  const float* guess0;
+  float* out;
+  int64_t maxiter;
+  float tol, eps;
+  int mode, has_noise;
+  double P_max, noise_sd;
+  uint64_t seed;
+  double* slab;          // [2][gridDim.x][2K+2]
+  unsigned* bar;         // [0] arrivals, [1] generation, [2] timeout flag (zeroed per call)
+  KState* st;
+};
+int resident_max_blocks(const PassCfg& cfg, int num_cu);
+hipError_t launch_resident(const PassCfg& cfg, int grid, const ResArgs& a, hipStream_t s);
+
 // Gram-space variant (gram.hip).  KT = K padded to 32-row tiles (0: unsupported).
 int gram_kt(int64_t K);
 size_t gram_slab_floats(int KT, int nb);

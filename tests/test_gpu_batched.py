@@ -40,7 +40,7 @@ def test_gm_batched_equals_single_calls():
     out, res = gm_batched(X, dict(opts, guess=p))
     for i in range(P):
         single = bz.gm(X[i], dict(opts, guess=p[i], seed=(99 + i * SEED_STRIDE) % 2 ** 64))
-        assert rel_l2(out[i].cpu().numpy(), single.cpu().numpy()) <= 1e-6
+        assert rel_l2(out[i].cpu().numpy(), single.cpu().numpy()) <= 1e-5
         assert res[i].iters == 30
 
 

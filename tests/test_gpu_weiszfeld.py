@@ -32,7 +32,7 @@ def _opts(meta, arr, dev="cuda"):
     return o
 
 
-@pytest.mark.parametrize("algo", ["auto", "twopass"])
+@pytest.mark.parametrize("algo", ["auto", "stream", "twopass"])
 @pytest.mark.parametrize("name", golden_names("gm2"))
 def test_gm2_matches_reference(name, algo):
     meta, arr = golden_case(name)
