@@ -74,6 +74,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   __shared__ double s_r[KMAX];
   __shared__ double s_fin[2][NW];
   __shared__ double s_tot[2];
+  __shared__ double s_part[NW * 64];
   __shared__ double scratch[16];
   __shared__ float s_anoise;
   __shared__ int s_ok;
@@ -167,21 +168,36 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   double last_mv = NAN;
   int conv = 0;
   for (;; ++it) {
-    // (1) reduce the previous pass's partials, same order in every block
-    const double* sl = a.slab + (int64_t)(it & 1) * nb * S;
-    for (int64_t k = tid; k < K; k += blockDim.x) {
-      double s1 = 0.0, s2 = 0.0;
-      for (unsigned b = 0; b < nb; ++b) {
-        s1 += sl[(int64_t)b * S + k];
-        if (it == 0) s2 += sl[(int64_t)b * S + K + k];
+    // (1) reduce the previous pass's partials, same order in every block: the
+    // slab columns needed (D2, at it = 0 also r, then mv2 / gn2) are spread over
+    // G thread groups that each sum every G-th block row; the G partials are
+    // then combined in LDS in group order (deterministic, and G loads in flight
+    // per column instead of nb dependent ones).
+    {
+      const double* sl = a.slab + (int64_t)(it & 1) * nb * S;
+      const int64_t ncol = (it == 0 ? 2 * K : K) + 2;      // [D2 | (r) | mv2 gn2]
+      const int64_t span = ncol <= 64 ? 64 : ncol <= 128 ? 128 : ncol <= 256 ? 256
+                          : ncol <= 512 ? 512 : 1024;
+      const int G = (int)(blockDim.x / span) > 0 ? (int)(blockDim.x / span) : 1;
+      for (int64_t col0 = 0; col0 < ncol; col0 += span) {
+        const int g = tid / (int)span;
+        const int64_t cc = col0 + tid % span;
+        const int64_t src = cc < ncol - 2 ? cc : 2 * K + (cc - (ncol - 2));
+        double s = 0.0;
+        if (g < G && cc < ncol)
+          for (unsigned b = g; b < nb; b += G) s += sl[(int64_t)b * S + src];
+        __syncthreads();
+        if (g < G) s_part[g * span + tid % span] = s;
+        __syncthreads();
+        if (tid < span && col0 + tid < ncol) {
+          double t = 0.0;
+          for (int gg = 0; gg < G; ++gg) t += s_part[gg * span + tid];
+          const int64_t c2 = col0 + tid;
+          if (c2 < K) s_d2[c2] = t;
+          else if (c2 < ncol - 2) s_r[c2 - K] = t;
+          else s_tot[c2 - (ncol - 2)] = t;
+        }
       }
-      s_d2[k] = s1;
-      if (it == 0) s_r[k] = s2;
-    }
-    if (tid < 2) {
-      double s = 0.0;
-      for (unsigned b = 0; b < nb; ++b) s += sl[(int64_t)b * S + 2 * K + tid];
-      s_tot[tid] = s;
     }
     __syncthreads();
     // (2) tol test of the pass that produced g_it (M:180-183)
