@@ -1,0 +1,260 @@
+"""The caller side of the aggregation boundary, device-resident.
+
+The reference's federated loop, `SGD` (MNIST_Air_weight.py:226-372), simulates
+K clients sequentially and hands the aggregator a CPU matrix built every step
+from per-client `.cpu()` copies (M:304, M:341) stacked by `flatten_list`
+(M:206-209), then copies the aggregate back parameter by parameter
+(M:354-358).  This module is the build's own counterpart:
+
+  * `ClientUpdates` (row f2): one preallocated [K, d] fp32 matrix on the
+    model's device; client k's parameters are written straight into row k
+    (no host round trip), and the aggregate is copied back into the
+    parameters through views — the layout is `flatten_list`'s (client-major,
+    `model.parameters()` order).
+  * `SGD` (row f4): the same signature, schedule, attacks, RNG consumption and
+    outputs as the reference loop, calling any aggregator with the reference's
+    `aggregate(wList, options)` contract (ours: `gm2`, `gm`, ...).
+  * `run` / `modelFactory` / `calculateAccuracy` / `getVarience`: the driver
+    pieces needed to produce records with the reference's keys and titles, so
+    draw.ipynb-style plots read them unchanged.
+
+Reference behaviours kept on purpose (pinned by tests/golden e2e fixtures):
+  * `model.state_dict()` aliases the parameters, so the reference's
+    "snapshot / recovery" around each client (M:290, M:343) restores nothing:
+    client k starts from client k-1's updated model, and the aggregator's guess
+    (M:349) is the model after the last client.
+  * classflip relabels y -> (C-1) - y as an integer (torch 1.1 semantics of
+    `9.0 - targets`, M:320; EMNIST: 61 - y); dataflip feeds 1 - x (M:326);
+    weightflip rewrites the last B rows as -w - 2*sum(honest)/B (M:380-383).
+  * OMA pre-noise is applied iff the aggregator is not `gm` and a variance is
+    given (M:351-352).
+"""
+from __future__ import annotations
+
+import os
+import pickle
+import random
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+__all__ = ["ClientUpdates", "SGD", "run", "modelFactory", "MLP", "setup_seed",
+           "calculateAccuracy", "getVarience", "classflip", "dataflip", "weightflip"]
+
+
+# ---- small pieces with the reference's semantics -------------------------------
+
+def setup_seed(seed):
+    """M:30-37."""
+    torch.manual_seed(seed)
+    torch.cuda.manual_seed(seed)
+    torch.cuda.manual_seed_all(seed)
+    np.random.seed(seed)
+    random.seed(seed)
+    torch.backends.cudnn.benchmark = False
+    torch.backends.cudnn.deterministic = True
+
+
+class MLP(nn.Module):
+    """The reference's linear model (M:53-61): 784 -> 10 (MNIST) or 784 -> 62 (EMNIST)."""
+
+    def __init__(self, input_size=784, output_size=10):
+        super().__init__()
+        self.linear = nn.Linear(input_size, output_size)
+
+    def forward(self, x):
+        return self.linear(x.view(x.size(0), -1))
+
+
+def _init_weights(m):
+    # M:92-95: xavier-normal with the ReLU gain, bias 0.01
+    if isinstance(m, (nn.Conv2d, nn.Linear)):
+        nn.init.xavier_normal_(m.weight, gain=nn.init.calculate_gain("relu"))
+        nn.init.constant_(m.bias, 0.01)
+
+
+def modelFactory(SEED=None, num_classes=10):  # noqa: N802 - reference name (M:98)
+    if SEED is not None:
+        setup_seed(SEED)
+    model = MLP(28 * 28, num_classes)
+    model.apply(_init_weights)
+    return model
+
+
+def calculateAccuracy(model, loss_func, loader, device):  # noqa: N802 - M:106-125
+    loss_sum, correct, total = 0.0, 0, 0
+    with torch.no_grad():
+        for xb, yb in loader:
+            xb, yb = xb.to(device), yb.to(device)
+            out = model(xb)
+            loss_sum += loss_func(out, yb).item() * len(yb)
+            correct += (out.argmax(dim=1) == yb).sum().item()
+            total += len(yb)
+    return loss_sum / total, correct / total
+
+
+def getVarience(w_local, honestSize):  # noqa: N802 - M:127-129 (one streaming pass)
+    h = w_local[:honestSize]
+    return torch.mean(((h - h.mean(dim=0)) ** 2).sum(dim=1))
+
+
+def classflip(messages, byzantinesize):
+    """The flip itself happens on the labels inside the loop (M:317-323)."""
+
+
+def dataflip(messages, byzantinesize):
+    """The flip itself happens on the inputs inside the loop (M:324-330)."""
+
+
+def weightflip(messages, byzantinesize):
+    """M:380-383, on the device matrix."""
+    honest_sum = messages[:-byzantinesize].sum(dim=0)
+    messages[-byzantinesize:].mul_(-1).add_(honest_sum / byzantinesize, alpha=-2)
+
+
+# ---- device-resident client packing (row f2) --------------------------------------
+
+class ClientUpdates:
+    """[K, d] matrix of client parameter vectors, resident on the model's device."""
+
+    def __init__(self, model: nn.Module, K: int, device=None):
+        self.params = list(model.parameters())
+        self.d = sum(p.numel() for p in self.params)
+        dev = device if device is not None else self.params[0].device
+        self.X = torch.empty(K, self.d, dtype=torch.float32, device=dev)
+
+    def flat(self, out=None):
+        """The model's parameters as one vector (flatten_list's row layout)."""
+        return torch.cat([p.detach().reshape(-1) for p in self.params], out=out)
+
+    def store(self, k: int):
+        self.flat(out=self.X[k])
+
+    def load(self, vector: torch.Tensor):
+        """Copy an aggregate back into the parameters (M:354-358) through views."""
+        off = 0
+        vector = vector.to(self.params[0].device)
+        with torch.no_grad():
+            for p in self.params:
+                n = p.numel()
+                p.copy_(vector[off:off + n].view_as(p))
+                off += n
+
+
+# ---- the federated loop (row f4) ---------------------------------------------------
+
+def _log(*k):
+    print(time.strftime("[%m-%d %H:%M:%S] ", time.localtime()), *k)
+    sys.stdout.flush()
+
+
+def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # noqa: N802
+        byzantineSize=0, attack=None, rounds=10, displayInterval=1000, SEED=None,
+        fixSeed=False, loss_func=None, train_dataset=None, validate_dataset=None, device=None,
+        batchSize=None, num_classes=10, verbose=True, **kw):
+    """Federated SGD with K = honest + Byzantine simulated clients (M:226-372)."""
+    assert byzantineSize == 0 or attack is not None
+    assert honestSize != 0
+    if fixSeed:
+        setup_seed(SEED)
+    K = honestSize + byzantineSize
+    device = device or torch.device("cpu")
+    DL = torch.utils.data.DataLoader
+
+    # contiguous data shards, one per client (M:238-239, M:253)
+    n = len(train_dataset)
+    cuts = [(i * n) // K for i in range(K + 1)]
+    shards = [torch.utils.data.Subset(train_dataset, range(cuts[i], cuts[i + 1])) for i in range(K)]
+    train_all = DL(dataset=train_dataset, batch_size=batchSize, pin_memory=True, shuffle=False)
+    val_all = DL(dataset=validate_dataset, batch_size=batchSize, pin_memory=True, shuffle=False)
+    draws = rounds * displayInterval * batchSize
+    samplers = [torch.utils.data.sampler.RandomSampler(s, num_samples=draws, replacement=True)
+                for s in shards]
+    streams = [iter(DL(dataset=shards[i], batch_size=batchSize, sampler=samplers[i]))
+               for i in range(K)]
+
+    tl, ta = calculateAccuracy(model, loss_func, train_all, device)
+    vl, va = calculateAccuracy(model, loss_func, val_all, device)
+    paths = {"train_loss": [tl], "train_acc": [ta], "val_loss": [vl], "val_acc": [va], "var": []}
+    if verbose:
+        _log(f"[0/{rounds}] train: loss={tl:.4f} acc={ta:.4f} val: loss={vl:.4f} acc={va:.4f}")
+
+    clients = ClientUpdates(model, K)
+    params = clients.params
+    attack_name = attack.__name__ if attack is not None else None
+    is_gm = aggregate.__name__ == "gm"
+    if noise_var is not None and not is_gm:
+        from .aggregators import OMA
+    for r in range(rounds):
+        for _ in range(displayInterval):
+            for node in range(K):
+                xb, yb = next(streams[node])
+                xb, yb = xb.to(device), yb.to(device)
+                if node >= honestSize and attack_name == "classflip":
+                    yb = (num_classes - 1) - yb          # integer relabel (M:320)
+                elif node >= honestSize and attack_name == "dataflip":
+                    xb = 1.0 - xb                         # M:326
+                loss = loss_func(model(xb), yb)
+                model.zero_grad()
+                loss.backward()
+                with torch.no_grad():
+                    for p in params:                      # M:302-303 / M:339-340
+                        p.add_(p.grad + weight_decay * p, alpha=-gamma)
+                clients.store(node)                       # row `node`, on the device
+            X = clients.X
+            if attack is not None:
+                attack(X, byzantineSize)
+            options = {"maxiter": 1000, "tol": 1e-5, "eta": 1, "noise_var": noise_var,
+                       "guess": clients.flat(), "honestSize": honestSize}     # M:349-350
+            if noise_var is not None and not is_gm:
+                OMA(X, noise_var)                         # M:351-352
+            clients.load(aggregate(X, options))           # M:353-358
+        paths["var"].append(getVarience(clients.X, honestSize).cpu())
+        tl, ta = calculateAccuracy(model, loss_func, train_all, device)
+        vl, va = calculateAccuracy(model, loss_func, val_all, device)
+        for key, v in (("train_loss", tl), ("train_acc", ta), ("val_loss", vl), ("val_acc", va)):
+            paths[key].append(v)
+        if verbose:
+            _log(f"[{r + 1}/{rounds}] train: loss={tl:.4f} acc={ta:.4f} "
+                 f"val: loss={vl:.4f} acc={va:.4f}")
+    return (model, paths["train_loss"], paths["train_acc"], paths["val_loss"], paths["val_acc"],
+            paths["var"])
+
+
+def run(optimizer, aggregate, attack, config, noise_var=None, dataSetConfig=None,  # noqa: N803
+        recordInFile=True, markOnTitle="", device=None, num_classes=10):
+    """Driver with the reference's record format and title naming (M:427-492)."""
+    cfg = dict(config)
+    if attack is None:
+        cfg["byzantineSize"] = 0
+    elif isinstance(attack, str):
+        attack = {"classflip": classflip, "dataflip": dataflip, "weightflip": weightflip}[attack]
+    cfg.update(aggregate=aggregate, attack=attack, noise_var=noise_var)
+    model = modelFactory(SEED=cfg["SEED"], num_classes=num_classes)
+    if device is not None and device != torch.device("cpu"):
+        model = nn.DataParallel(model)   # the reference's class name in titles (NB:25)
+    model = model.to(device or torch.device("cpu"))
+    attack_name = "baseline" if attack is None else attack.__name__
+    title = "{}_{}_{}_{}".format(model.__class__.__name__, optimizer.__name__, attack_name,
+                                 aggregate.__name__)
+    if noise_var is not None:
+        title += "_" + str(noise_var)
+    if markOnTitle:
+        title += "_" + markOnTitle
+    res = optimizer(model, device=device, num_classes=num_classes, **cfg)
+    _, tl, ta, vl, va, var = res
+    record = dict(dataSetConfig or {})
+    for key, val in cfg.items():
+        if key in ("train_dataset", "validate_dataset"):
+            continue
+        record[key] = val.__class__.__name__ if callable(val) else val
+    record.update(trainLossPath=tl, trainAccPath=ta, valLossPath=vl, valAccPath=va,
+                  variencePath=var)
+    if recordInFile:
+        os.makedirs(os.path.dirname(cfg["CACHE_DIR"] + title) or ".", exist_ok=True)
+        with open(cfg["CACHE_DIR"] + title, "wb") as f:
+            pickle.dump(record, f)
+    return title, record

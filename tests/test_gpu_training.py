@@ -1,0 +1,75 @@
+"""The device-resident training-loop counterpart (rows f2, f4) vs the reference's
+own SGD loop, pinned by the golden end-to-end fixtures (tests/golden: the
+reference's SGD, M:226-372, run on a synthetic MNIST-shaped set)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_case, rel_l2
+
+pytestmark = pytest.mark.gpu
+
+
+def synthetic_mnist(seed, n):
+    # same recipe as tests/golden/make_golden.py
+    proto = np.random.default_rng(600).standard_normal((10, 1, 28, 28)).astype(np.float32)
+    r = np.random.default_rng(seed)
+    y = r.integers(0, 10, n).astype(np.int64)
+    x = (proto[y] + 2.0 * r.standard_normal((n, 1, 28, 28))).astype(np.float32)
+    return torch.from_numpy(x), torch.from_numpy(y)
+
+
+def _run(agg_name, device, monkeypatch):
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd import training as T
+    meta, arr = golden_case(f"e2e_sgd_classflip_{agg_name}")
+    if agg_name == "gm":
+        monkeypatch.setenv("BYZ_AIRCOMP_NOISE", "host")   # replay the reference's draws
+    tr = torch.utils.data.TensorDataset(*synthetic_mnist(601, 2000))
+    va = torch.utils.data.TensorDataset(*synthetic_mnist(602, 500))
+    model = T.modelFactory(SEED=2021).to(device)
+    agg = getattr(bz, agg_name)
+    res = T.SGD(model, gamma=1e-2, aggregate=agg, weight_decay=0.0, noise_var=meta["noise_var"],
+                honestSize=45, byzantineSize=5, attack=T.classflip, rounds=2, displayInterval=2,
+                SEED=2021, fixSeed=True, loss_func=torch.nn.CrossEntropyLoss(),
+                train_dataset=tr, validate_dataset=va, device=torch.device(device),
+                batchSize=50, verbose=False)
+    m, tl, ta, vl, vacc, var = res
+    w = torch.cat([p.detach().flatten().cpu() for p in m.parameters()]).numpy()
+    return meta, arr, w, tl, ta, vl, vacc, var
+
+
+@pytest.mark.parametrize("agg_name", ["gm2", "gm"])
+def test_loop_with_cpu_model_matches_reference(agg_name, monkeypatch):
+    """Model on CPU like the fixture; only the aggregation runs on the GPU."""
+    meta, arr, w, tl, ta, vl, vacc, var = _run(agg_name, "cpu", monkeypatch)
+    assert rel_l2(w, arr["weights"]) <= 1e-5
+    np.testing.assert_allclose(tl, meta["trainLossPath"], rtol=1e-5)
+    np.testing.assert_allclose(vl, meta["valLossPath"], rtol=1e-5)
+    assert ta == meta["trainAccPath"] and vacc == meta["valAccPath"]
+    np.testing.assert_allclose([float(v) for v in var], meta["variencePath"], rtol=1e-4)
+
+
+@pytest.mark.parametrize("agg_name", ["gm2", "gm"])
+def test_loop_device_resident_matches_reference(agg_name, monkeypatch):
+    """Model, client matrix and aggregation all on the GPU (no host round trip)."""
+    meta, arr, w, tl, ta, vl, vacc, var = _run(agg_name, "cuda", monkeypatch)
+    assert rel_l2(w, arr["weights"]) <= 1e-4
+    np.testing.assert_allclose(tl, meta["trainLossPath"], rtol=1e-4)
+    np.testing.assert_allclose(vl, meta["valLossPath"], rtol=1e-4)
+
+
+def test_client_updates_layout_is_flatten_list():
+    from byzantine_aircomp_amd import training as T
+    m = T.MLP(784, 10).cuda()
+    cu = T.ClientUpdates(m, 3)
+    for k in range(3):
+        with torch.no_grad():
+            for p in m.parameters():
+                p.add_(1.0)
+        cu.store(k)
+    want = torch.cat([p.detach().flatten() for p in m.parameters()])
+    assert torch.equal(cu.X[2], want)
+    assert cu.X.shape == (3, 7850) and cu.X.device.type == "cuda"
+    cu.load(torch.zeros(7850, device="cuda"))
+    assert all(float(p.abs().sum()) == 0 for p in m.parameters())

@@ -1,0 +1,77 @@
+"""Host logic of the training-loop counterpart (row f4), on CPU.
+
+With the CPU oracle standing in for the aggregator, the build's `SGD`
+(byzantine_aircomp_amd/training.py) must reproduce the reference's own loop
+bit for bit on the golden end-to-end fixtures: data sharding and sampling, RNG
+consumption, the integer classflip, the parameter update, the aliasing
+"snapshot", the guess, the OMA gate and the records.  (The GPU variant of this
+test, tests/test_gpu_training.py, swaps in the HIP aggregators.)
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_case
+from oracle import aggregators as orc
+from test_gpu_training import synthetic_mnist
+
+
+def _as_aggregator(name):
+    fn = {"gm2": lambda w, o={}: orc.gm2(w, o)[0], "gm": lambda w, o={}: orc.gm(w, o)[0]}[name]
+    fn.__name__ = name
+    return fn
+
+
+@pytest.mark.parametrize("agg_name", ["gm2", "gm"])
+def test_sgd_counterpart_bit_exact_with_reference(agg_name):
+    from byzantine_aircomp_amd import training as T
+    meta, arr = golden_case(f"e2e_sgd_classflip_{agg_name}")
+    tr = torch.utils.data.TensorDataset(*synthetic_mnist(601, 2000))
+    va = torch.utils.data.TensorDataset(*synthetic_mnist(602, 500))
+    model = T.modelFactory(SEED=2021)
+    res = T.SGD(model, gamma=1e-2, aggregate=_as_aggregator(agg_name), weight_decay=0.0,
+                noise_var=meta["noise_var"], honestSize=45, byzantineSize=5,
+                attack=T.classflip, rounds=2, displayInterval=2, SEED=2021, fixSeed=True,
+                loss_func=torch.nn.CrossEntropyLoss(), train_dataset=tr, validate_dataset=va,
+                device=torch.device("cpu"), batchSize=50, verbose=False)
+    m, tl, ta, vl, vacc, var = res
+    w = torch.cat([p.detach().flatten() for p in m.parameters()]).numpy()
+    assert np.array_equal(w, arr["weights"])
+    assert tl == meta["trainLossPath"] and vl == meta["valLossPath"]
+    assert ta == meta["trainAccPath"] and vacc == meta["valAccPath"]
+    assert [float(v) for v in var] == meta["variencePath"]
+
+
+def test_weightflip_on_device_matrix_semantics():
+    from byzantine_aircomp_amd import training as T
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(10, 33, generator=g)
+    ref = X.clone()
+    s = torch.sum(ref[0:-3], dim=0)                 # M:381-383
+    ref[-3:].mul_(-1)
+    ref[-3:].add_(s / 3, alpha=-2)
+    T.weightflip(X, 3)
+    assert torch.equal(X, ref)
+
+
+def test_run_writes_reference_record(tmp_path):
+    import pickle
+    from byzantine_aircomp_amd import training as T
+    tr = torch.utils.data.TensorDataset(*synthetic_mnist(601, 400))
+    va = torch.utils.data.TensorDataset(*synthetic_mnist(602, 100))
+    cfg = {"honestSize": 8, "byzantineSize": 2, "rounds": 1, "displayInterval": 1,
+           "weight_decay": 0.0, "fixSeed": True, "SEED": 2021, "batchSize": 50, "shuffle": True,
+           "gamma": 1e-2, "CACHE_DIR": str(tmp_path) + "/mnist_K10_B2_",
+           "train_dataset": tr, "validate_dataset": va,
+           "loss_func": torch.nn.CrossEntropyLoss()}
+    title, rec = T.run(T.SGD, _as_aggregator("gm2"), "classflip", cfg,
+                       dataSetConfig={"name": "mnist", "dataSet": "mnist",
+                                      "dataSetSize": 400, "maxFeature": 784},
+                       device=torch.device("cpu"))
+    assert title == "MLP_SGD_classflip_gm2"              # M:446-451 naming
+    with open(cfg["CACHE_DIR"] + title, "rb") as f:
+        saved = pickle.load(f)                           # our own file
+    for key in ("trainLossPath", "trainAccPath", "valLossPath", "valAccPath", "variencePath",
+                "honestSize", "byzantineSize", "aggregate", "attack", "name"):
+        assert key in saved
+    assert saved["aggregate"] == "function" and len(saved["valLossPath"]) == 2
