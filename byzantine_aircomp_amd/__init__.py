@@ -8,6 +8,7 @@ HIP kernels for gfx950 behind a C ABI (include/gmagg.h, libgmagg.so):
 See DESIGN.md for the kernels and INTEGRATION.md for swapping them into the
 reference's training loop.
 """
-from .aggregators import GMResult, OMA, context, gm, gm2  # noqa: F401
+from .aggregators import (GMResult, Krum, OMA, context, gm, gm2, mean, median,  # noqa: F401
+                          trimmed_mean)
 
 __version__ = "0.1.0"

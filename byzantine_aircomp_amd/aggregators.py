@@ -41,7 +41,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["gm2", "gm", "OMA", "GMResult", "last_result", "Context", "context"]
+__all__ = ["gm2", "gm", "OMA", "mean", "median", "trimmed_mean", "Krum", "GMResult",
+           "last_result", "Context", "context"]
 
 
 @dataclass
@@ -239,6 +240,50 @@ def gm2(wList, options={}):  # noqa: B006 - the reference's signature (M:162)
 def gm(wList, options={}):  # noqa: B006 - the reference's signature (M:131)
     """AirComp Weiszfeld geometric median (MNIST_Air_weight.py:131-160)."""
     return _weiszfeld(wList, options, aircomp=True)
+
+
+def _coordinate(wList, fn_name, *extra):
+    X = _stage(wList)
+    X, ldx = _rows(X)
+    K, d = X.shape
+    out = torch.empty(d, dtype=torch.float32, device=X.device)
+    ctx = context(X.device)
+    with torch.cuda.device(X.device):
+        _lib.check(getattr(ctx.lib, fn_name)(ctx.handle, X.data_ptr(), K, d, ldx, *extra,
+                                             out.data_ptr(), _stream_ptr(X.device)), fn_name)
+    return out if wList.device == out.device else out.to(wList.device)
+
+
+def mean(wList, options={}):  # noqa: B006 - reference signature (M:186)
+    """Column mean (MNIST_Air_weight.py:186-187)."""
+    return _coordinate(wList, "gm_mean_f32")
+
+
+def median(wList, options={}):  # noqa: B006 - reference signature (M:194)
+    """Coordinate-wise lower median, torch.median semantics (M:194-195)."""
+    return _coordinate(wList, "gm_median_f32")
+
+
+def trimmed_mean(wList, options={}):  # noqa: B006 - reference signature (M:189)
+    """Coordinate-wise mean without the int(0.1 K) smallest and largest (M:189-192)."""
+    return _coordinate(wList, "gm_trimmed_mean_f32", int(wList.shape[0] * 0.1))
+
+
+def Krum(wList, options):  # noqa: N802 - reference name (M:197)
+    """The row with the smallest sum of squared distances to its honestSize-1
+    nearest rows, itself included (M:197-204)."""
+    X = _stage(wList)
+    X, ldx = _rows(X)
+    K, d = X.shape
+    out = torch.empty(d, dtype=torch.float32, device=X.device)
+    idx = C.c_int64()
+    ctx = context(X.device)
+    with torch.cuda.device(X.device):
+        _lib.check(ctx.lib.gm_krum_f32(ctx.handle, X.data_ptr(), K, d, ldx,
+                                       int(options["honestSize"]), out.data_ptr(), C.byref(idx),
+                                       _stream_ptr(X.device)), "gm_krum_f32")
+    Krum.last_index = idx.value
+    return out if wList.device == out.device else out.to(wList.device)
 
 
 def OMA(message, noise_var=0.01, noise_source=None, seed=None):  # noqa: N802 - reference name

@@ -166,16 +166,18 @@ bool pick_cfg(int64_t K, int V, int64_t ldx, PassCfg* cfg) {
   else if (K <= 1024) { lpr = 8; r = 8; }
   else if (K <= 2048) { lpr = 4; r = 8; }
   else return false;
-  // GMAGG_PASS_CFG="NW,LPR,R" forces a tile (tuning runs); it must cover K.
+  int occ = 1;
+  // GMAGG_PASS_CFG="NW,LPR,R[,OCC]" forces a tile (tuning runs); it must cover K.
   if (const char* e = getenv("GMAGG_PASS_CFG")) {
-    int a = 0, b = 0, c2 = 0;
-    if (sscanf(e, "%d,%d,%d", &a, &b, &c2) == 3 && (int64_t)a * (64 / b) * c2 >= K) {
-      nw = a; lpr = b; r = c2;
+    int a = 0, b = 0, c2 = 0, o = 1;
+    const int n = sscanf(e, "%d,%d,%d,%d", &a, &b, &c2, &o);
+    if (n >= 3 && b > 0 && (int64_t)a * (64 / b) * c2 >= K) {
+      nw = a; lpr = b; r = c2; occ = n == 4 ? o : 1;
     }
   }
   // lane offsets are 32-bit: (rows per wave - 1) * ldx + ldx must fit in bytes
   if ((uint64_t)(64 / lpr) * (uint64_t)ldx * 4u >= (1ull << 32)) return false;
-  *cfg = PassCfg{V, nw, lpr, r};
+  *cfg = PassCfg{V, nw, lpr, r, occ};
   return pass_cfg_supported(*cfg);
 }
 
@@ -731,6 +733,56 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
   if (results)
     for (int64_t p = 0; p < P; ++p)
       results[p] = gm_result{hst[p].iters, hst[p].last_movement, hst[p].converged, GM_ALGO_STREAM};
+  return GM_OK;
+}
+
+int gm_mean_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, float* out,
+                void* stream) {
+  if (!c || !X || !out || K < 1 || d < 0 || ldx < d) return fail(GM_ERR_INVALID, "gm_mean_f32: bad args");
+  if (d == 0) return GM_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(launch_col_mean(X, K, d, ldx, out, reinterpret_cast<hipStream_t>(stream)));
+  return GM_OK;
+}
+
+int gm_median_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, float* out,
+                  void* stream) {
+  if (!c || !X || !out || K < 1 || d < 0 || ldx < d) return fail(GM_ERR_INVALID, "gm_median_f32: bad args");
+  if (K > 256) return fail(GM_ERR_UNSUPPORTED, "gm_median_f32: K <= 256");
+  if (d == 0) return GM_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(launch_col_select(X, K, d, ldx, 0, 0, out, reinterpret_cast<hipStream_t>(stream)));
+  return GM_OK;
+}
+
+int gm_trimmed_mean_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
+                        int64_t trim, float* out, void* stream) {
+  if (!c || !X || !out || K < 1 || d < 0 || ldx < d || trim < 0 || 2 * trim >= K)
+    return fail(GM_ERR_INVALID, "gm_trimmed_mean_f32: bad args");
+  if (K > 256) return fail(GM_ERR_UNSUPPORTED, "gm_trimmed_mean_f32: K <= 256");
+  if (d == 0) return GM_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(launch_col_select(X, K, d, ldx, 1, trim, out, reinterpret_cast<hipStream_t>(stream)));
+  return GM_OK;
+}
+
+int gm_krum_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, int64_t honest,
+                float* out, int64_t* index, void* stream) {
+  if (!c || !X || !out || K < 1 || d < 0 || ldx < d || honest < 2 || honest - 1 > K)
+    return fail(GM_ERR_INVALID, "gm_krum_f32: bad args (needs 2 <= honestSize <= K+1)");
+  if (K > 1024) return fail(GM_ERR_UNSUPPORTED, "gm_krum_f32: K <= 1024");
+  HIPCHK(hipSetDevice(c->device));
+  Workspace w;
+  int rc = ensure_ws(c, 1, 1, 1, &w, 0, (int)K);          // G area holds the K x K distances
+  if (rc) return rc;
+  int64_t* didx = reinterpret_cast<int64_t*>(w.sums);
+  HIPCHK(launch_krum(X, K, d, ldx, honest - 1, w.G, out, didx,
+                     reinterpret_cast<hipStream_t>(stream)));
+  if (index) {
+    HIPCHK(hipMemcpyAsync(index, didx, sizeof(int64_t), hipMemcpyDeviceToHost,
+                          reinterpret_cast<hipStream_t>(stream)));
+    HIPCHK(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+  }
   return GM_OK;
 }
 

@@ -25,6 +25,7 @@ struct alignas(64) KState {
 // per thread (the block covers NW*(64/LPR)*R rows).
 struct PassCfg {
   int V, NW, LPR, R;
+  int OCC = 1;   // blocks per CU the kernel's registers are capped for
 };
 
 struct PassArgs {
@@ -115,6 +116,14 @@ hipError_t launch_gram(const float* X, int64_t K, int64_t d, int64_t ldx, const 
 hipError_t launch_gram_solve(const double* G, int KP, int64_t K, int64_t maxiter, float tol,
                              float eps, double* alpha, double* u, float* coef, KState* st,
                              hipStream_t s);
+
+// Other aggregators (coordinate.hip).
+hipError_t launch_col_mean(const float* X, int64_t K, int64_t d, int64_t ldx, float* out,
+                           hipStream_t s);
+hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, int mode,
+                             int64_t b, float* out, hipStream_t s);
+hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t kk, double* D,
+                       float* out, int64_t* index, hipStream_t s);
 
 // OMA / synthetic fills (oma.hip).
 hipError_t launch_oma_apply(float* X, int64_t K, int64_t d, int64_t ldx, const float* hr,

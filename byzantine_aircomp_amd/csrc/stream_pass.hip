@@ -36,8 +36,10 @@ struct Tile {
 
 // MODE: 0 step, 1 init, 2 init + ||x_k||^2.  PIPE: chunk c+1's loads are in
 // flight while chunk c is reduced (two tiles of registers).
-template <int V, int NW, int LPR, int R, int MODE, bool PIPE>
-__global__ void __launch_bounds__(NW * 64) weiszfeld_pass(PassArgs a) {
+// OCC: blocks per CU the register budget is capped for (2 -> <= 64 VGPRs at
+// 16 waves); with OCC > 1 the row weights are read from LDS instead of VGPRs.
+template <int V, int NW, int LPR, int R, int MODE, bool PIPE, int OCC = 1>
+__global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs a) {
   constexpr bool SUM_ONLY = MODE == 3;     // closing pass of the Gram variant: g = sum c_k x_k
   constexpr bool INIT = MODE == 1 || MODE == 2;
   constexpr bool WANT_R = MODE == 2;
@@ -51,6 +53,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_pass(PassArgs a) {
   __shared__ float s_red[NW][J];
   __shared__ float s_g[J];
   __shared__ double s_fin[2][NW];
+  __shared__ float s_w[OCC > 1 ? NW * QW * R : 1];
 
   if (gridDim.y > 1) {                       // batched independent problems
     const int64_t pb = blockIdx.y;
@@ -82,11 +85,16 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_pass(PassArgs a) {
   }
   const uint32_t loff = (uint32_t)q * (uint32_t)a.ldx;
 
-  float wt[R];
+  float wt[OCC > 1 ? 1 : R];
   float a_noise = 0.f;
   if constexpr (!INIT) {
+    if constexpr (OCC > 1) {
+      for (int k = tid; k < NRG * R; k += NW * 64) s_w[k] = k < K ? a.coef[k] : 0.f;
+      __syncthreads();
+    } else {
 #pragma unroll
-    for (int i = 0; i < R; ++i) wt[i] = rval[i] ? a.coef[rg + NRG * i] : 0.f;
+      for (int i = 0; i < R; ++i) wt[i] = rval[i] ? a.coef[rg + NRG * i] : 0.f;
+    }
     a_noise = a.st->a_noise;
   }
 
@@ -134,9 +142,13 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_pass(PassArgs a) {
 #pragma unroll
       for (int v = 0; v < V; ++v) acc[v] = 0.f;
 #pragma unroll
-      for (int i = 0; i < R; ++i)
+      for (int i = 0; i < R; ++i) {
+        float wi;
+        if constexpr (OCC > 1) wi = s_w[rg + NRG * i];
+        else wi = wt[i];
 #pragma unroll
-        for (int v = 0; v < V; ++v) acc[v] = fmaf(wt[i], t.x[i][v], acc[v]);
+        for (int v = 0; v < V; ++v) acc[v] = fmaf(wi, t.x[i][v], acc[v]);
+      }
       // ... over the wave's row groups ...
 #pragma unroll
       for (int o = LPR; o < 64; o <<= 1)
@@ -268,39 +280,41 @@ static int pass_variant() {
 }
 #endif
 
-template <int V, int NW, int LPR, int R, int MODE>
+template <int V, int NW, int LPR, int R, int MODE, int OCC>
 static const void* pass_fn() {
-  // Measured on MI355X (profiles/r01_ab_pass.txt): the plain pass is as fast or
-  // faster at every K; the two-tile variant spills at R*V = 32 and gains
-  // nothing at R*V <= 16, so it is only built with -DGMK_PIPE_VARIANT for A/B runs.
+  // Measured on MI355X (profiles/r01_ab_pass.txt, r01_pipe_sweep.txt): the plain
+  // pass is as fast or faster at every K, so the two-tile variant is only built
+  // with -DGMK_PIPE_VARIANT for A/B runs.
 #ifdef GMK_PIPE_VARIANT
   if (pass_variant() == 1)
-    return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, true>);
+    return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, true, OCC>);
 #endif
-  return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, false>);
+  return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, false, OCC>);
 }
 
-template <int V, int NW, int LPR, int R>
+template <int V, int NW, int LPR, int R, int OCC>
 static const void* pass_fn_mode(int mode) {
   switch (mode) {
-    case 0: return pass_fn<V, NW, LPR, R, 0>();
-    case 1: return pass_fn<V, NW, LPR, R, 1>();
-    case 2: return pass_fn<V, NW, LPR, R, 2>();
-    default: return pass_fn<V, NW, LPR, R, 3>();
+    case 0: return pass_fn<V, NW, LPR, R, 0, OCC>();
+    case 1: return pass_fn<V, NW, LPR, R, 1, OCC>();
+    case 2: return pass_fn<V, NW, LPR, R, 2, OCC>();
+    default: return pass_fn<V, NW, LPR, R, 3, OCC>();
   }
 }
 
-// (waves per block, lanes per row segment, rows per thread) tiles built.
+// (waves per block, lanes per row segment, rows per thread, blocks per CU) tiles built.
 #define GMK_FOR_EACH_CFG(X_, V_)                                                             \
-  X_(V_, 16, 64, 1) X_(V_, 16, 64, 2) X_(V_, 16, 64, 4) X_(V_, 16, 64, 8) X_(V_, 16, 32, 8)  \
-  X_(V_, 16, 16, 8) X_(V_, 16, 8, 8) X_(V_, 16, 4, 8) X_(V_, 16, 4, 4) X_(V_, 16, 16, 4)     \
-  X_(V_, 8, 8, 16) X_(V_, 8, 4, 8) X_(V_, 8, 16, 8) X_(V_, 8, 8, 8) X_(V_, 4, 8, 8)          \
-  X_(V_, 4, 16, 4) X_(V_, 8, 32, 4)
+  X_(V_, 16, 64, 1, 1) X_(V_, 16, 64, 2, 1) X_(V_, 16, 64, 4, 1) X_(V_, 16, 64, 8, 1)        \
+  X_(V_, 16, 32, 8, 1) X_(V_, 16, 16, 8, 1) X_(V_, 16, 8, 8, 1) X_(V_, 16, 4, 8, 1)          \
+  X_(V_, 16, 4, 4, 1) X_(V_, 16, 16, 4, 1) X_(V_, 8, 8, 16, 1) X_(V_, 8, 4, 8, 1)            \
+  X_(V_, 8, 16, 8, 1) X_(V_, 8, 8, 8, 1) X_(V_, 4, 8, 8, 1) X_(V_, 4, 16, 4, 1)              \
+  X_(V_, 8, 32, 4, 1) X_(V_, 16, 8, 8, 2) X_(V_, 16, 16, 16, 1) X_(V_, 8, 8, 16, 2)          \
+  X_(V_, 16, 32, 8, 2) X_(V_, 16, 64, 4, 2)
 
 static const void* pass_kernel(const PassCfg& cfg, int mode) {
-#define GMK_CASE(V_, W_, L_, R_)                                                    \
-  if (cfg.V == V_ && cfg.NW == W_ && cfg.LPR == L_ && cfg.R == R_)                  \
-    return pass_fn_mode<V_, W_, L_, R_>(mode);
+#define GMK_CASE(V_, W_, L_, R_, O_)                                                 \
+  if (cfg.V == V_ && cfg.NW == W_ && cfg.LPR == L_ && cfg.R == R_ && cfg.OCC == O_) \
+    return pass_fn_mode<V_, W_, L_, R_, O_>(mode);
   GMK_FOR_EACH_CFG(GMK_CASE, 4)
   GMK_FOR_EACH_CFG(GMK_CASE, 2)
   GMK_FOR_EACH_CFG(GMK_CASE, 1)

@@ -133,6 +133,20 @@ int gm_weiszfeld_batched_f32(gm_ctx* ctx, const float* X, int64_t P, int64_t K, 
                              float* out, int64_t ldo, const gm_opts* opts, gm_result* results,
                              void* stream);
 
+/* The reference's other aggregators (MNIST_Air_weight.py:186-204), out[d]:
+ *   gm_mean_f32          mean(wList, options)          M:186-187
+ *   gm_median_f32        median(wList, options)        M:194-195 (lower median), K <= 256
+ *   gm_trimmed_mean_f32  trimmed_mean(wList, options)  M:189-192, trim = int(0.1 K) per end, K <= 256
+ *   gm_krum_f32          Krum(wList, options)          M:197-204, K <= 1024; *index = chosen row */
+int gm_mean_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t ldx, float* out,
+                void* stream);
+int gm_median_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t ldx, float* out,
+                  void* stream);
+int gm_trimmed_mean_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t ldx,
+                        int64_t trim, float* out, void* stream);
+int gm_krum_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t ldx,
+                int64_t honest_size, float* out, int64_t* index, void* stream);
+
 /* OMA(message, noise_var): in-place per-client equalised AWGN
  * (MNIST_Air_weight.py:385-394), draws from on-device Philox keyed by `seed`. */
 int gm_oma_philox_f32(gm_ctx* ctx, float* X, int64_t K, int64_t d, int64_t ldx,

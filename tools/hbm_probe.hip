@@ -41,6 +41,52 @@ __global__ void read_sum(const f4* __restrict__ p, size_t n4, float* sink) {
   if (acc == 1234.5f) *sink = acc;  // never true for zero-filled input; keeps loads live
 }
 
+// The streaming pass's access pattern without its arithmetic: a block reads a
+// chunk of J columns (LPR = J/4 lanes x 16 B per row) of all K rows (rows
+// ldx floats apart), grid-striding over chunks.  Isolates what row-segment
+// width and row count cost the memory system.
+template <int LPR, int R>
+__global__ void __launch_bounds__(1024) tile_read(const float* __restrict__ X, int K, size_t d,
+                                                 size_t ldx, float* sink) {
+  constexpr int QW = 64 / LPR, NRG = 16 * QW, J = LPR * 4;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c = lane % LPR, q = lane / LPR, rg = w * QW + q;
+  const size_t nch = (d + J - 1) / J;
+  float acc = 0.f;
+  for (size_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    const size_t col = ch * J + c * 4;
+    f4 v[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int k = rg + NRG * i;
+      v[i] = (k < K && col < d) ? __builtin_nontemporal_load(
+                                      reinterpret_cast<const f4*>(X + (size_t)k * ldx + col))
+                                : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc += v[i].x + v[i].y + v[i].z + v[i].w;
+  }
+  if (acc == 1234.5f) *sink = acc;
+}
+
+template <int LPR, int R>
+static double run_tile(const float* X, int K, size_t d, float* sink, int blocks) {
+  hipEvent_t a, b;
+  CHK(hipEventCreate(&a));
+  CHK(hipEventCreate(&b));
+  hipLaunchKernelGGL((tile_read<LPR, R>), dim3(blocks), dim3(1024), 0, 0, X, K, d, d, sink);
+  CHK(hipDeviceSynchronize());
+  const int reps = 5;
+  CHK(hipEventRecord(a));
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL((tile_read<LPR, R>), dim3(blocks), dim3(1024), 0, 0, X, K, d, d, sink);
+  CHK(hipEventRecord(b));
+  CHK(hipEventSynchronize(b));
+  float ms = 0.f;
+  CHK(hipEventElapsedTime(&ms, a, b));
+  return (double)K * d * 4.0 * reps / (ms * 1e-3) / 1e9;
+}
+
 template <int U, bool NT>
 static double run(const f4* p, size_t n4, float* sink, int blocks, int threads) {
   hipEvent_t a, b;
@@ -87,5 +133,21 @@ int main(int argc, char** argv) {
     }
   }
   printf("{\"probe\": \"hbm_read\", \"bytes\": %zu, \"best_GBps\": %.1f}\n", bytes, best);
+  // tile patterns over a K=1000 x d=11M matrix (the C3 shape) and K=256 x 15.6M (C4 shard)
+  const float* X = reinterpret_cast<const float*>(p);
+  for (int bpc : {1, 2}) {
+    const int blocks = cus * bpc;
+    printf("tile K=1000 d=11M blocks/CU=%d: J=16 %.0f  J=32 %.0f  J=64 %.0f  J=128 %.0f  J=256 %.0f GB/s\n",
+           bpc, run_tile<4, 4>(X, 1000, 11000000, sink, blocks),
+           run_tile<8, 8>(X, 1000, 11000000, sink, blocks),
+           run_tile<16, 16>(X, 1000, 11000000, sink, blocks),
+           run_tile<32, 32>(X, 1000, 11000000, sink, blocks),
+           run_tile<64, 64>(X, 1000, 11000000, sink, blocks));
+    printf("tile K=256 d=15.6M blocks/CU=%d: J=32 %.0f  J=64 %.0f  J=128 %.0f  J=256 %.0f GB/s\n",
+           bpc, run_tile<8, 2>(X, 256, 15625000, sink, blocks),
+           run_tile<16, 4>(X, 256, 15625000, sink, blocks),
+           run_tile<32, 8>(X, 256, 15625000, sink, blocks),
+           run_tile<64, 16>(X, 256, 15625000, sink, blocks));
+  }
   return 0;
 }
