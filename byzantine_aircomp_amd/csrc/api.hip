@@ -156,17 +156,18 @@ int allreduce(gm_ctx* c, double* buf, int64_t n, hipStream_t s) {
 // R rows each cover K.  Bigger K -> narrower chunk, so a block's tile (and the
 // bytes it has in flight) stays ~64-128 KiB.
 bool pick_cfg(int64_t K, int V, int64_t ldx, PassCfg* cfg) {
-  int nw = 16, lpr, r;
+  int nw = 16, lpr, r, occ = 1;
   if (K <= 16) { lpr = 64; r = 1; }
   else if (K <= 32) { lpr = 64; r = 2; }
   else if (K <= 64) { lpr = 64; r = 4; }
   else if (K <= 128) { lpr = 64; r = 8; }
   else if (K <= 256) { lpr = 32; r = 8; }
   else if (K <= 512) { lpr = 16; r = 8; }
-  else if (K <= 1024) { lpr = 8; r = 8; }
+  // K <= 1024: two 512-thread blocks per CU, each with a 1024 x 32 tile (128 B row
+  // segments): 6.29 vs 6.05 TB/s for one 1024-thread block (profiles/r01_occ_sweep.txt)
+  else if (K <= 1024) { nw = 8; lpr = 8; r = 16; occ = 2; }
   else if (K <= 2048) { lpr = 4; r = 8; }
   else return false;
-  int occ = 1;
   // GMAGG_PASS_CFG="NW,LPR,R[,OCC]" forces a tile (tuning runs); it must cover K.
   if (const char* e = getenv("GMAGG_PASS_CFG")) {
     int a = 0, b = 0, c2 = 0, o = 1;
