@@ -80,7 +80,9 @@ def pmc_traffic(workload):
     data = json.load(open(files[-1]))
     for name, row in data["kernels"].items():
         m = re.search(r"weiszfeld_pass<([^>]*)>", name)
-        if m and m.group(1).split(", ")[-2] == "0":
+        targs = m.group(1).split(", ") if m else []
+        mode = targs[4] if len(targs) == 7 else (targs[-2] if targs else None)   # <V,NW,LPR,R,MODE,PIPE,OCC>
+        if mode == "0":
             return row["hbm_bytes_per_launch"] / 1e9, os.path.relpath(files[-1], ROOT)
     return None, None
 
