@@ -44,6 +44,7 @@ WORKLOADS = {
     "c2": (50, 7850, 10),                   # MNIST MLP d, K=50, B=10 (use --agg gm --var 1e-2)
 }
 MFMA_F32_PEAK_TFLOPS = 157.3                 # v_mfma_f32_32x32x2_f32, dense (MI355X_MICROARCH.md)
+MFMA_BF16_PEAK_TFLOPS = 2516.6               # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz, dense
 
 
 def parse():
@@ -52,7 +53,7 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
-    p.add_argument("--algo", default="auto", choices=["auto", "stream", "twopass", "gram"])
+    p.add_argument("--algo", default="auto", choices=["auto", "stream", "twopass", "gram", "gram_f32"])
     p.add_argument("--agg", default="gm2", choices=["gm2", "gm"])
     p.add_argument("--var", type=float, default=None, help="gm noise variance (None = no AWGN)")
     p.add_argument("--maxiter", type=int, default=1000)
@@ -176,18 +177,29 @@ def main():
         avg_pass_s = (pass_ms / 1e3) / max(launches, 1)
         achieved = per_launch_bytes / avg_pass_s / 1e9
         traffic, traffic_src = pmc_traffic(args.workload) if world == 1 else (None, None)
-        if res.algo == "gram":
-            # dominant kernel = gram_partial: MFMA-bound; FLOPs issued = upper-triangle
-            # 32x32 tiles of the K-padded Gram, 2 FLOP per MAC, d_local columns
+        if res.algo in ("gram", "gram_f32"):
+            # dominant kernel = the Gram partial: upper-triangle 32x32 tiles of the
+            # K-padded Gram, 2 FLOP per MAC, d_local columns; the split kernel issues
+            # 4 bf16 MFMAs (hh, hm, mh, mm) per tile and 16 columns.  It also reads X
+            # once: price both ceilings and report the binding one.
             kt = 1 if K <= 32 else 2 if K <= 64 else 4 if K <= 128 else 8
-            flops = kt * (kt + 1) / 2 * 1024 * 2.0 * d
+            split = res.algo == "gram"
+            flops = kt * (kt + 1) / 2 * 1024 * 2.0 * d * (4 if split else 1)
+            peak = MFMA_BF16_PEAK_TFLOPS if split else MFMA_F32_PEAK_TFLOPS
             tf = flops / avg_pass_s / 1e12
-            roof = {"bound": "mfma", "achieved": tf, "peak": MFMA_F32_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": tf / MFMA_F32_PEAK_TFLOPS, "traffic": None,
-                    "kernel": "gram_partial (v_mfma_f32_32x32x2_f32, upper-triangle tiles)",
-                    "launches_timed": launches, "avg_launch_us": avg_pass_s * 1e6,
-                    "algorithmic_flops_per_launch": flops,
-                    "syrk_flops_per_launch (2*K^2*d)": 2.0 * K * K * d}
+            gbs = per_launch_bytes / avg_pass_s / 1e9
+            mf = {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s",
+                  "frac": tf / peak, "traffic": None}
+            hb = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": gbs / HBM_PEAK_GBS, "traffic": None}
+            roof, other = (mf, hb) if mf["frac"] >= hb["frac"] else (hb, mf)
+            roof.update({"kernel": ("gram_split_partial (v_mfma_f32_32x32x16_bf16, h+m split, "
+                                    "upper-triangle tiles)") if split else
+                                   "gram_partial (v_mfma_f32_32x32x2_f32, upper-triangle tiles)",
+                         "launches_timed": launches, "avg_launch_us": avg_pass_s * 1e6,
+                         "algorithmic_flops_per_launch": flops,
+                         "algorithmic_bytes_per_launch": per_launch_bytes,
+                         "other_ceiling": other})
         else:
             roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -214,7 +226,7 @@ def main():
                                    + (f", noise_var {args.var}" if args.agg == "gm" else ""),
                        "K": K, "d": d_total, "byzantine": B, "iters": res.iters,
                        "algo": res.algo, "parallelism": f"d-shard x{world}" if world > 1 else "none",
-                       "passes_per_aggregation": res.iters + 1 if res.algo != "gram" else 2},
+                       "passes_per_aggregation": 2 if res.algo.startswith("gram") else res.iters + 1},
             "roofline": roof,
             "cpu_baseline": None,
         }

@@ -17,6 +17,7 @@ ABI_VERSION = 1
 GM_MODE_IDEAL, GM_MODE_AIRCOMP = 0, 1
 GM_NOISE_PHILOX, GM_NOISE_HOST = 0, 1
 GM_ALGO_AUTO, GM_ALGO_STREAM, GM_ALGO_TWOPASS, GM_ALGO_GRAM, GM_ALGO_RESIDENT = 0, 1, 2, 3, 4
+GM_ALGO_GRAM_F32 = 5
 
 NOISE_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.POINTER(C.c_float),
                        C.POINTER(C.c_float), C.POINTER(C.c_float))

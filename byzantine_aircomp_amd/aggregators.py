@@ -56,7 +56,7 @@ class GMResult:
 last_result: GMResult | None = None
 _ALGOS = {"auto": _lib.GM_ALGO_AUTO, "stream": _lib.GM_ALGO_STREAM,
           "twopass": _lib.GM_ALGO_TWOPASS, "gram": _lib.GM_ALGO_GRAM,
-          "resident": _lib.GM_ALGO_RESIDENT}
+          "resident": _lib.GM_ALGO_RESIDENT, "gram_f32": _lib.GM_ALGO_GRAM_F32}
 _ALGO_NAMES = {v: k for k, v in _ALGOS.items()}
 
 

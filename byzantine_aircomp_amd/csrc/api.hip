@@ -60,6 +60,7 @@ struct gm_ctx {
   char* host = nullptr;   // pinned: KState mirror + host-noise staging
   size_t host_bytes = 0;
   bool timing = false;
+  hipEvent_t poll_ev[2] = {nullptr, nullptr};   // lagged convergence polls
   std::vector<hipEvent_t> ev_free;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used;
 };
@@ -257,19 +258,42 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
 
 // Gram-space gm2 (gram.hip): G = X'X'^T once (MFMA), the Weiszfeld loop in K-space
 // (one launch, fp64), one closing pass g = sum_k a_k x_k.  Two reads of X.
+//
+// AUTO guard (guarded = true).  The K-space loop is exact up to the error of G
+// (fp32 accumulation; for the bf16 split also the bits of x' beyond h + m), and
+// it has none of the reference's fp32 rounding of the iterate.  The closing pass
+// is then a full streaming STEP pass at the returned weights, which also yields
+// the exact distances ||x_k - g||^2; gram_verify compares the next weights from
+// those with the K-space map's and measures the one-step error e = ||X'^T b||.
+// The result is kept only if (1) e / (1 - rho) <= 1e-6 ||g|| (rho = the last
+// K-space contraction ratio, clamped to [0.5, 0.95]), and (2) the reference's own
+// movement noise floor, measured at 0.4-1.8 x 2^-24 ||g||, is
+// below tol/3, so that the reference stops within +-1 iteration of the exact
+// loop.  Otherwise *rejected is set and the caller runs the streaming path.
 int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const float* guess0,
-             float* out, const gm_opts* o, gm_result* res, const PassCfg& cfg, hipStream_t s) {
+             float* out, const gm_opts* o, gm_result* res, const PassCfg& cfg, hipStream_t s,
+             bool split, bool guarded, bool* rejected) {
+  *rejected = false;
   const int KT = gram_kt(K), KP = 32 * KT;
-  const int nb_g = std::max(1, std::min(4 * c->num_cu, (int)((d + 4095) / 4096)));
+  int nb_g;
+  if (split) {   // ~8K columns per block, whole rounds of one block per CU
+    nb_g = (int)std::max<int64_t>(1, (d + 8191) / 8192);
+    if (nb_g > c->num_cu) nb_g = (nb_g + c->num_cu - 1) / c->num_cu * c->num_cu;
+  } else {
+    nb_g = std::max(1, std::min(4 * c->num_cu, (int)((d + 4095) / 4096)));
+  }
+  const int64_t cpb = gram_cols_per_block(d, nb_g, split);
+  nb_g = (int)std::max<int64_t>(1, (d + cpb - 1) / cpb);
   const int J = cfg.LPR * cfg.V;
   const int nb_p = (int)std::max<int64_t>(
       1, std::min<int64_t>((d + J - 1) / J, (int64_t)c->num_cu * pass_blocks_per_cu(cfg, 3)));
   Workspace w;
-  int rc = ensure_ws(c, K, d, 1, &w, gram_slab_floats(KT, nb_g), KP);
+  int rc = ensure_ws(c, K, d, nb_p, &w, gram_slab_floats(KT, nb_g), KP);
   if (rc) return rc;
-  rc = ensure_host(c, sizeof(KState));
+  rc = ensure_host(c, sizeof(KState) + 4 * sizeof(double));
   if (rc) return rc;
   KState* hst = reinterpret_cast<KState*>(c->host);
+  double* hsums = reinterpret_cast<double*>(c->host + sizeof(KState));
   HIPCHK(hipMemsetAsync(w.st, 0, sizeof(KState), s));
   // centre p = guess0, staged to an aligned workspace copy (float4 loads)
   float* p = w.g[1];
@@ -277,25 +301,46 @@ int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const
   hipEvent_t e0, e1;
   rc = record_pass_begin(c, s, &e0, &e1);
   if (rc) return rc;
-  HIPCHK(launch_gram(X, K, d, ldx, p, nb_g, w.gslab, w.G, s));
+  HIPCHK(launch_gram(X, K, d, ldx, p, nb_g, w.gslab, w.G, s, split));
   rc = record_pass_end(c, s, e0, e1);
   if (rc) return rc;
   rc = allreduce(c, w.G, (int64_t)KP * KP, s);
   if (rc) return rc;
   HIPCHK(launch_gram_solve(w.G, KP, K, o->maxiter, (float)o->tol, (float)o->eps, w.alpha, w.u,
                            w.coef, w.st, s));
+  // closing pass: g = sum_k a_k x_k (+ the exact distances to g when guarded)
+  const int64_t S = guarded ? K + 2 : 2;
   PassArgs a{};
   a.X = X; a.K = K; a.d = d; a.ldx = ldx;
   a.g_old = p; a.g_new = out; a.coef = w.coef; a.st = w.st;
-  a.slab = w.slab; a.slab_stride = 0;
-  HIPCHK(launch_pass(cfg, 3, nb_p, a, s));
+  a.slab = w.slab; a.slab_stride = S;
+  HIPCHK(launch_pass(cfg, guarded ? 0 : 3, nb_p, a, s));
+  HIPCHK(launch_slab_reduce(w.slab, nb_p, S, w.sums, w.st, s));   // [D (K)] [||p-g||^2, ||g||^2]
+  rc = allreduce(c, w.sums, S, s);
+  if (rc) return rc;
+  if (guarded)
+    HIPCHK(launch_gram_verify(w.G, KP, K, (float)o->eps, w.u, w.alpha, w.sums, w.r, w.st, s));
   HIPCHK(hipMemcpyAsync(hst, w.st, sizeof(KState), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hsums, w.sums + (S - 2), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (guarded) {
+    const double u = std::ldexp(1.0, -24);
+    const double gn = std::sqrt(std::max(0.0, hsums[1]));
+    double rho = hst->guard_r;
+    rho = rho != rho ? 0.5 : std::min(0.95, std::max(0.5, rho));
+    const double pred = hst->guard_q / (1.0 - rho) / gn;
+    const bool accurate = pred <= 1e-6;                     // NaN fails
+    const bool floor_ok = !hst->converged || 2.0 * u * gn <= o->tol / 3.0;
+    if (!accurate || !floor_ok) {
+      *rejected = true;
+      return GM_OK;
+    }
+  }
   gm_result r{};
   r.iters = hst->iters;
   r.last_movement = hst->last_movement;
   r.converged = hst->converged;
-  r.algo_used = GM_ALGO_GRAM;
+  r.algo_used = split ? GM_ALGO_GRAM : GM_ALGO_GRAM_F32;
   if (res) *res = r;
   return GM_OK;
 }
@@ -329,6 +374,8 @@ int gm_ctx_destroy(gm_ctx* c) {
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->ws) (void)hipFree(c->ws);
   if (c->host) (void)hipHostFree(c->host);
+  for (auto e : c->poll_ev)
+    if (e) (void)hipEventDestroy(e);
   for (auto e : c->ev_free) (void)hipEventDestroy(e);
   for (auto& p : c->ev_used) {
     (void)hipEventDestroy(p.first);
@@ -422,12 +469,15 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   PassCfg cfg{};
   int algo = o->algo;
   const int V = pick_vec(X, d, ldx);
-  // AUTO: Gram-space for gm2 at K <= 256 on large d (MI355X, profiles/r01_cmp_algos.txt:
-  // K=256 x d=15.6M 69.1 vs 56.0 aggregations/s; X read twice instead of n+1 times),
-  // streaming otherwise.
+  // AUTO: Gram-space (split bf16) for gm2 at K <= 256 on large d, kept if its
+  // accuracy guard passes (run_gram); streaming otherwise.  X is read twice
+  // instead of n+1 times (profiles/r01_cmp_algos.txt, r02_gram_split.txt).
   if (algo == GM_ALGO_AUTO && o->mode == GM_MODE_IDEAL && gram_kt(K) > 0 && V == 4 &&
-      d >= (int64_t)1 << 18 && pick_cfg(K, V, ldx, &cfg))
-    algo = GM_ALGO_GRAM;
+      d >= (int64_t)1 << 18 && ldx < ((int64_t)1 << 26) && pick_cfg(K, V, ldx, &cfg)) {
+    bool rejected = false;
+    const int rc0 = run_gram(c, X, K, d, ldx, guess0, out, o, res, cfg, s, true, true, &rejected);
+    if (rc0 || !rejected) return rc0;
+  }
   // Small problems: the register-resident single launch when every chunk fits one
   // co-resident block (unsharded, Philox or no noise).
   const bool host_noise_req = o->mode == GM_MODE_AIRCOMP && o->noise_source == GM_NOISE_HOST;
@@ -446,14 +496,17 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       return fail(GM_ERR_UNSUPPORTED, "streaming pass supports K <= 2048 (K=%lld)", (long long)K);
     else algo = GM_ALGO_TWOPASS;
   }
-  if (algo == GM_ALGO_GRAM) {
+  if (algo == GM_ALGO_GRAM || algo == GM_ALGO_GRAM_F32) {
     if (o->mode != GM_MODE_IDEAL)
       return fail(GM_ERR_UNSUPPORTED, "Gram variant is gm2 only (AirComp noise leaves span(X))");
     if (gram_kt(K) == 0 || V != 4 || !pick_cfg(K, V, ldx, &cfg))
       return fail(GM_ERR_UNSUPPORTED, "Gram variant needs K <= 256, d and ldx multiples of 4, "
                   "16-byte aligned X (K=%lld d=%lld ldx=%lld)", (long long)K, (long long)d,
                   (long long)ldx);
-    return run_gram(c, X, K, d, ldx, guess0, out, o, res, cfg, s);
+    // the split kernel addresses a 16-row group with 32-bit lane offsets
+    const bool split = algo == GM_ALGO_GRAM && ldx < ((int64_t)1 << 26);
+    bool rejected = false;
+    return run_gram(c, X, K, d, ldx, guess0, out, o, res, cfg, s, split, false, &rejected);
   }
   if (algo != GM_ALGO_STREAM && algo != GM_ALGO_TWOPASS)
     return fail(GM_ERR_INVALID, "unknown algo %d", o->algo);
@@ -475,10 +528,12 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   int rc = ensure_ws(c, K, d, nb, &w);
   if (rc) return rc;
   const bool host_noise = o->mode == GM_MODE_AIRCOMP && o->noise_source == GM_NOISE_HOST;
-  rc = ensure_host(c, sizeof(KState) + sizeof(float) * (2 * K + d_total + 1) + 256);
+  const size_t host_ks = align_up(3 * sizeof(KState), 256);   // final + two lagged slots
+  rc = ensure_host(c, host_ks + sizeof(float) * (2 * K + d_total + 1) + 256);
   if (rc) return rc;
   KState* hst = reinterpret_cast<KState*>(c->host);
-  float* h_hr = reinterpret_cast<float*>(c->host + align_up(sizeof(KState), 256));
+  KState* hslot = hst + 1;
+  float* h_hr = reinterpret_cast<float*>(c->host + host_ks);
   float* h_hi = h_hr + K;
   float* h_n = h_hi + K;   // d_total + 1
   HIPCHK(hipMemsetAsync(w.st, 0, sizeof(KState), s));
@@ -560,6 +615,14 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   int check_every = o->check_every;
   if (check_every <= 0) check_every = (K * d >= (int64_t)1 << 24) ? 1 : 16;
   if (host_noise) check_every = 1;
+  // Polling every iteration (large passes): read iteration t-1's state while
+  // iteration t is already queued, so the device never waits for the host.  If
+  // t-1 stopped the loop, iteration t's launches see `done` and exit at once.
+  const bool lagged = check_every == 1 && !host_noise;
+  if (lagged)
+    for (auto& e : c->poll_ev)
+      if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  int64_t pending = -1;   // iteration whose KState copy is in flight (lagged)
 
   int64_t t = 0;
   for (; t < o->maxiter; ++t) {
@@ -585,6 +648,16 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
     ka.do_check = 1;
     ka.do_coef = last ? 0 : 1;
     HIPCHK(launch_kspace(ka, s));
+    if (lagged && !last) {
+      HIPCHK(hipMemcpyAsync(&hslot[t & 1], w.st, sizeof(KState), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipEventRecord(c->poll_ev[t & 1], s));
+      if (pending >= 0) {
+        HIPCHK(hipEventSynchronize(c->poll_ev[pending & 1]));
+        if (hslot[pending & 1].done) break;
+      }
+      pending = t;
+      continue;
+    }
     if (last || (t + 1) % check_every == 0) {
       rc = poll(hst);
       if (rc) return rc;

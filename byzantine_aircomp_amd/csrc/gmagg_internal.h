@@ -17,7 +17,10 @@ struct alignas(64) KState {
   double last_movement;  // fp32 movement of the last body, widened
   float a_noise;         // scale of the per-column noise in the next pass (AIRCOMP)
   float s;               // scaler sqrt(mean(g^2)) of the current iterate (AIRCOMP)
-  double pad[4];
+  // Gram variant, written by gram_solve for the AUTO accuracy guard (api.hip):
+  double guard_q;        // ||X'^T b||: one-step error of the K-space map (gram_verify)
+  double guard_r;        // last / previous K-space movement (contraction estimate)
+  double pad[2];
 };
 
 // Streaming pass configuration: V floats per lane per row, NW waves per
@@ -109,10 +112,16 @@ int resident_max_blocks(const PassCfg& cfg, int num_cu);
 hipError_t launch_resident(const PassCfg& cfg, int grid, const ResArgs& a, hipStream_t s);
 
 // Gram-space variant (gram.hip).  KT = K padded to 32-row tiles (0: unsupported).
+// split = true: bf16 h+m split on v_mfma_f32_32x32x16_bf16 (default);
+// false: exact f32-input v_mfma_f32_32x32x2_f32.
 int gram_kt(int64_t K);
 size_t gram_slab_floats(int KT, int nb);
+int64_t gram_cols_per_block(int64_t d, int nb, bool split);
 hipError_t launch_gram(const float* X, int64_t K, int64_t d, int64_t ldx, const float* p, int nb,
-                       float* slab, double* G, hipStream_t s);
+                       float* slab, double* G, hipStream_t s, bool split);
+hipError_t launch_gram_verify(const double* G, int KP, int64_t K, float eps, const double* u,
+                              const double* alpha, const double* Dx, double* bvec, KState* st,
+                              hipStream_t s);
 hipError_t launch_gram_solve(const double* G, int KP, int64_t K, int64_t maxiter, float tol,
                              float eps, double* alpha, double* u, float* coef, KState* st,
                              hipStream_t s);

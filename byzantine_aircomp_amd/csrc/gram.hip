@@ -15,6 +15,8 @@
 // KT-1-w (KT+1 tiles: balanced), so for KT = 8 each of the 4 waves issues 9
 // MFMAs per 2 columns.  Blocks own disjoint column ranges; fp32 partials per
 // block go to a slab that gram_reduce sums in fp64 (fixed order).
+#include <algorithm>
+
 #include "device_util.h"
 #include "gmagg_internal.h"
 
@@ -148,18 +150,253 @@ __global__ void __launch_bounds__(256) gram_partial(const float* __restrict__ X,
   }
 }
 
-// Sum the fp32 block partials in fp64 (fixed order) and unpack the upper
-// triangle into a full symmetric G[KP][KP].  Element e of a tile: register
-// reg = e / 64, lane = e % 64 -> row (reg&3) + 8*(reg>>2) + 4*(lane>>5), col lane&31.
-__global__ void __launch_bounds__(256) gram_reduce(const float* __restrict__ slab, int nb,
-                                                   int KT, double* __restrict__ G) {
+// ---------------------------------------------------------------------------
+// Split-bf16 Gram (the default Gram path).  Each centred element is split as
+// x' = h + m with h = bf16(x'), m = bf16(x' - h): h + m carries 16 significant
+// bits and every bf16 x bf16 product is exact in fp32, so
+//   G = (h+m)(h+m)^T = hh^T + hm^T + mh^T + mm^T
+// costs four v_mfma_f32_32x32x16_bf16 per 32x32 tile and 16 columns: 1/4 of the
+// issue cycles of the f32-input MFMA.  Dropping mm^T (three products) is NOT
+// enough: for rows that nearly coincide the m parts are coherent and mm^T is a
+// 2^-16-relative bias on D (measured: 2.5e-4 relative error on a tight
+// cluster).  What is left — the bits of x' beyond h + m (<= 2^-17 |x'|) and fp32
+// accumulation — is priced at run time by the AUTO guard (api.hip, run_gram).
+//
+// Block: 256 threads; stage = 64 columns x KP rows, loaded as float4 by all
+// threads (16 B per row segment, 16 rows per wave instruction), centred, split
+// and written as bf16 h/m images [KP][72] (144-B rows: conflict-free
+// ds_read_b128 fragment reads).  Two stages of LDS: the global loads of stage
+// s+1 are in flight under stage s's MFMAs; one barrier per stage.  Blocks own
+// disjoint column ranges of ~8K columns; fp32 partials per block are summed in
+// fp64 by gram_reduce (single-level accumulation over <= cpb/4 MFMA steps).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kSplitBK = 64;                // columns per stage
+constexpr int kSplitLS = kSplitBK + 8;      // LDS row stride (bf16): 144 B
+
+// Tile t of wave W at compile time (same map as wave_tile).
+template <int KT, int W, int T>
+struct SplitTile {
+  static constexpr int first = KT - W;
+  static constexpr int a = KT == 1 ? 0 : (T < first ? W : KT - 1 - W);
+  static constexpr int b = KT == 1 ? 0 : (T < first ? W + T : KT - 1 - W + (T - first));
+};
+
+template <int KT, int W, int T>
+__device__ __forceinline__ void split_tile_mfma(const bf16x8 (&fh)[KT], const bf16x8 (&fm)[KT],
+                                                f32x16 (&acc)[GramShape<KT>::PER_WAVE]) {
+  if constexpr (T < GramShape<KT>::PER_WAVE) {
+    constexpr int a = SplitTile<KT, W, T>::a, b = SplitTile<KT, W, T>::b;
+    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fh[a], fh[b], acc[T], 0, 0, 0);
+    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fh[a], fm[b], acc[T], 0, 0, 0);
+    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fm[a], fh[b], acc[T], 0, 0, 0);
+    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fm[a], fm[b], acc[T], 0, 0, 0);
+    split_tile_mfma<KT, W, T + 1>(fh, fm, acc);
+  }
+}
+
+// Split Gram block: 512 threads = 4 MFMA waves (consumers, one compile-time
+// specialisation per wave) + 4 staging waves (producers).  A producer thread
+// owns 16-byte row segments of a 64-column stage (rows r0 + 16 i, column group
+// cg) and keeps TWO stages of loads in flight in two register sets (set = stage
+// parity, static after unrolling the stage loop by 2): while the consumers run
+// stage s from LDS buffer s&1, the producers centre/split/store stage s+1 into
+// buffer (s+1)&1 and re-issue the freed set for stage s+3.  One barrier per
+// stage.  ~128 KiB of loads in flight per CU instead of 64.
+template <int KT>
+struct SplitProducer {
+  static constexpr int RPT = GramShape<KT>::ROWS_PER_THREAD;
+  const float* X;
+  const float* p;
+  int64_t K, ldx, c_begin, c_end;
+  int r0, cg;
+  uint32_t lrow;
+  f32x4 st[2][RPT];
+  f32x4 pc[2];
+  bool cval[2];
+
+  // Every load is issued unconditionally (rows >= K read a real row, columns
+  // past c_end read column 0 of the stage) and the padding is applied at commit
+  // time — a select at load time lets the compiler turn the load into a branch.
+  template <int SET>
+  __device__ __forceinline__ void fetch(int s) {
+    const int64_t c0 = c_begin + (int64_t)s * kSplitBK;
+    cval[SET] = c0 + cg * 4 < c_end;
+    const uint32_t lc = cval[SET] ? (uint32_t)(cg * 4) : 0u;
+    pc[SET] = *reinterpret_cast<const f32x4*>(p + c0 + lc);
+    const float* xs = X + c0;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int64_t rb = 16 * i < K ? 16 * i : 0;      // wave-uniform, always a real row
+      const uint32_t off = (r0 + 16 * i < K ? lrow : 0u) + lc;
+      st[SET][i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(xs + rb * ldx + off));
+    }
+  }
+  template <int SET>
+  __device__ __forceinline__ void commit(__bf16* Lh, __bf16* Lm) {   // centre, split, store
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int r = r0 + 16 * i;
+      const f32x4 x = (cval[SET] && r < K) ? st[SET][i] - pc[SET] : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x2 x01 = {x[0], x[1]}, x23 = {x[2], x[3]};
+      const bf16x2 h01 = __builtin_convertvector(x01, bf16x2);
+      const bf16x2 h23 = __builtin_convertvector(x23, bf16x2);
+      const f32x2 r01 = x01 - __builtin_convertvector(h01, f32x2);
+      const f32x2 r23 = x23 - __builtin_convertvector(h23, f32x2);
+      const bf16x2 m01 = __builtin_convertvector(r01, bf16x2);
+      const bf16x2 m23 = __builtin_convertvector(r23, bf16x2);
+      *reinterpret_cast<bf16x4*>(Lh + r * kSplitLS + cg * 4) = bf16x4{h01[0], h01[1], h23[0], h23[1]};
+      *reinterpret_cast<bf16x4*>(Lm + r * kSplitLS + cg * 4) = bf16x4{m01[0], m01[1], m23[0], m23[1]};
+    }
+  }
+};
+
+template <int KT>
+__device__ __forceinline__ void split_producer(const float* __restrict__ X, int64_t K,
+                                               int64_t ldx, const float* __restrict__ p,
+                                               int64_t c_begin, int64_t c_end, int nstage,
+                                               __bf16 (*lds)[2][GramShape<KT>::KP * kSplitLS]) {
+  SplitProducer<KT> P;
+  const int t = threadIdx.x - 256;
+  P.X = X; P.p = p; P.K = K; P.ldx = ldx; P.c_begin = c_begin; P.c_end = c_end;
+  P.r0 = t >> 4; P.cg = t & 15;
+  P.lrow = (uint32_t)P.r0 * (uint32_t)ldx;
+  // prologue: stage 0 -> buffer 0, stages 1 (set 1) and 2 (set 0) in flight
+  if (nstage > 0) P.template fetch<0>(0);
+  if (nstage > 1) P.template fetch<1>(1);
+  if (nstage > 0) P.template commit<0>(lds[0][0], lds[0][1]);
+  if (nstage > 2) P.template fetch<0>(2);
+  __syncthreads();
+  for (int s = 0; s < nstage; s += 2) {
+    // stage s runs on the consumers; commit s+1 (set 1), re-issue set 1 for s+3
+    if (s + 1 < nstage) P.template commit<1>(lds[1][0], lds[1][1]);
+    if (s + 3 < nstage) P.template fetch<1>(s + 3);
+    __syncthreads();
+    if (s + 1 >= nstage) break;
+    // stage s+1 runs; commit s+2 (set 0), re-issue set 0 for s+4
+    if (s + 2 < nstage) P.template commit<0>(lds[0][0], lds[0][1]);
+    if (s + 4 < nstage) P.template fetch<0>(s + 4);
+    __syncthreads();
+  }
+}
+
+// Consumer wave W (W < 0: idle slot for KT < 8): per 16-column step it reads the
+// h/m fragments of row tiles W..KT-1 once (one ds_read_b128 each) and issues 4
+// MFMAs per tile, all registers statically indexed.
+template <int KT, int W>
+__device__ __forceinline__ void split_consumer(int nstage, float* __restrict__ slab,
+                                               __bf16 (*lds)[2][GramShape<KT>::KP * kSplitLS]) {
+  using Sh = GramShape<KT>;
+  constexpr int NT = Sh::PER_WAVE;
+  constexpr bool MMA = W >= 0;
+  constexpr int LO = KT == 1 ? 0 : (W < 0 ? 0 : W);
+  const int lane = threadIdx.x & 63;
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+  const int fo = (lane & 31) * kSplitLS + (lane >> 5) * 8;   // fragment offset in a tile
+  __syncthreads();                                           // stage 0 is in buffer 0
+  for (int s = 0; s < nstage; ++s) {
+    if constexpr (MMA) {
+      const __bf16* Lh = lds[s & 1][0];
+      const __bf16* Lm = lds[s & 1][1];
+#pragma unroll
+      for (int ks = 0; ks < kSplitBK / 16; ++ks) {
+        bf16x8 fh[KT], fm[KT];
+#pragma unroll
+        for (int t = LO; t < KT; ++t) {
+          fh[t] = *reinterpret_cast<const bf16x8*>(Lh + t * 32 * kSplitLS + ks * 16 + fo);
+          fm[t] = *reinterpret_cast<const bf16x8*>(Lm + t * 32 * kSplitLS + ks * 16 + fo);
+        }
+        split_tile_mfma<KT, (W < 0 ? 0 : W), 0>(fh, fm, acc);
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (MMA) {
+    float* out = slab + (int64_t)blockIdx.x * Sh::TILES * 1024;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      int a, b;
+      wave_tile<KT>(W, t, a, b);
+      float* o = out + tri_index(a, b, KT) * 1024;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) o[e * 64 + lane] = acc[t][e];
+    }
+  }
+}
+
+template <int KT>
+__global__ void __launch_bounds__(512, 1) gram_split_partial(const float* __restrict__ X,
+                                                             int64_t K, int64_t d, int64_t ldx,
+                                                             const float* __restrict__ p,
+                                                             int64_t cols_per_block,
+                                                             float* __restrict__ slab) {
+  __shared__ __bf16 lds[2][2][GramShape<KT>::KP * kSplitLS];   // [buffer][h|m]
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t c_begin = (int64_t)blockIdx.x * cols_per_block;
+  const int64_t c_end = c_begin + cols_per_block < d ? c_begin + cols_per_block : d;
+  const int nstage = c_begin < c_end ? (int)((c_end - c_begin + kSplitBK - 1) / kSplitBK) : 0;
+  if (w >= 4) {
+    split_producer<KT>(X, K, ldx, p, c_begin, c_end, nstage, lds);
+    return;
+  }
+  if constexpr (KT == 8) {
+    switch (w) {
+      case 0: split_consumer<KT, 0>(nstage, slab, lds); break;
+      case 1: split_consumer<KT, 1>(nstage, slab, lds); break;
+      case 2: split_consumer<KT, 2>(nstage, slab, lds); break;
+      default: split_consumer<KT, 3>(nstage, slab, lds); break;
+    }
+  } else if constexpr (KT == 4) {
+    switch (w) {
+      case 0: split_consumer<KT, 0>(nstage, slab, lds); break;
+      case 1: split_consumer<KT, 1>(nstage, slab, lds); break;
+      default: split_consumer<KT, -1>(nstage, slab, lds); break;
+    }
+  } else {
+    if (w == 0) split_consumer<KT, 0>(nstage, slab, lds);
+    else split_consumer<KT, -1>(nstage, slab, lds);
+  }
+}
+
+// Sum the fp32 block partials in fp64 in a fixed order, in two steps so that
+// every element has many loads in flight: gram_reduce_part sums blocks
+// y, y+NG, y+2NG, ... (four interleaved fp64 chains, combined in order) into
+// tmp[y][e]; gram_reduce_final adds tmp[0..NG) and unpacks the upper triangle
+// into a full symmetric G[KP][KP].  Element e of a tile: register reg = e / 64,
+// lane = e % 64 -> row (reg&3) + 8*(reg>>2) + 4*(lane>>5), col lane&31.
+constexpr int kReduceGroups = 32;
+
+__global__ void __launch_bounds__(256) gram_reduce_part(const float* __restrict__ slab, int nb,
+                                                        int64_t n, double* __restrict__ tmp) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int y = blockIdx.y, NG = gridDim.y;
+  if (e >= n) return;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  int b = y, i = 0;
+  for (; b + 3 * NG < nb; b += 4 * NG) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] += (double)slab[(int64_t)(b + u * NG) * n + e];
+  }
+  for (; b < nb; b += NG, ++i) acc[i & 3] += (double)slab[(int64_t)b * n + e];
+  tmp[(int64_t)y * n + e] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+}
+
+__global__ void __launch_bounds__(256) gram_reduce_final(const double* __restrict__ tmp, int NG,
+                                                         int KT, double* __restrict__ G) {
   const int tiles = KT * (KT + 1) / 2;
   const int64_t n = (int64_t)tiles * 1024;
   const int KP = 32 * KT;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     double s = 0.0;
-    for (int b = 0; b < nb; ++b) s += (double)slab[(int64_t)b * n + e];
+    for (int y = 0; y < NG; ++y) s += tmp[(int64_t)y * n + e];
     const int tix = (int)(e >> 10), el = (int)(e & 1023);
     int a = 0;
     while (tri_index(a, KT - 1, KT) < tix) ++a;        // row tile of this triangle index
@@ -187,7 +424,7 @@ __global__ void __launch_bounds__(1024) gram_solve(const double* __restrict__ G,
   double aTu = 0.0;
   __syncthreads();
   int64_t it = 0;
-  double last_mv = NAN;
+  double last_mv = NAN, prev_mv = NAN;
   int conv = 0;
   for (; it < maxiter; ++it) {
     // next weights from D_k = G_kk - 2 u_k + a^T u   (clamped at 0 against cancellation)
@@ -222,6 +459,7 @@ __global__ void __launch_bounds__(1024) gram_solve(const double* __restrict__ G,
     const double mv2 = block_sum(part_mv, scratch);
     aTu = block_sum(part_atu, scratch);
     const float mv = (float)sqrt(mv2 > 0.0 ? mv2 : (mv2 != mv2 ? mv2 : 0.0));
+    prev_mv = last_mv;
     last_mv = (double)mv;
     if (tid == 0) s_stop = mv <= tol ? 1 : 0;
     __syncthreads();
@@ -231,8 +469,58 @@ __global__ void __launch_bounds__(1024) gram_solve(const double* __restrict__ G,
     st->iters = it;
     st->last_movement = last_mv;
     st->converged = conv;
+    st->guard_r = last_mv / prev_mv;   // contraction estimate for the AUTO guard (NaN if 1 step)
     st->done = 0;   // let the closing pass run
   }
+}
+
+// A posteriori check of the Gram path (AUTO guard, api.hip run_gram).  The
+// closing pass was a full streaming STEP pass at the returned weights a, so
+// `Dx` holds the exact ||x_k - g||^2 (fp32 elements, fp64 sums, as the
+// streaming path computes them).  Compare the next Weiszfeld weights from the
+// exact distances with those the K-space loop would take (from G): the
+// difference b is the one-step error of the K-space map at g, and its size in
+// R^d is sqrt(b^T G b).  Writes it to st->guard_q.  One block.
+__global__ void __launch_bounds__(1024) gram_verify(const double* __restrict__ G, int KP, int64_t K,
+                                                    float eps, const double* __restrict__ u,
+                                                    const double* __restrict__ alpha,
+                                                    const double* __restrict__ Dx,
+                                                    double* __restrict__ bvec, KState* st) {
+  __shared__ double scratch[16];
+  const int tid = threadIdx.x;
+  double atu = 0.0;
+  for (int64_t k = tid; k < K; k += blockDim.x) atu += alpha[k] * u[k];
+  atu = block_sum(atu, scratch);
+  double wg = 0.0, wx = 0.0;
+  for (int64_t k = tid; k < K; k += blockDim.x) {
+    const double Dg = G[k * KP + k] - 2.0 * u[k] + atu;
+    wg += 1.0 / (double)clamp_dist(Dg > 0.0 ? Dg : (Dg != Dg ? Dg : 0.0), eps);
+    wx += 1.0 / (double)clamp_dist(Dx[k], eps);
+  }
+  const double Wg = block_sum(wg, scratch), Wx = block_sum(wx, scratch);
+  for (int64_t k = tid; k < K; k += blockDim.x) {
+    const double Dg = G[k * KP + k] - 2.0 * u[k] + atu;
+    bvec[k] = (1.0 / (double)clamp_dist(Dg > 0.0 ? Dg : (Dg != Dg ? Dg : 0.0), eps)) / Wg -
+              (1.0 / (double)clamp_dist(Dx[k], eps)) / Wx;
+  }
+  __syncthreads();
+  double q = 0.0;
+  for (int64_t k0 = tid >> 2; k0 < K; k0 += blockDim.x >> 2) {
+    double sacc = 0.0;
+    for (int64_t j = tid & 3; j < K; j += 4) sacc += G[k0 * KP + j] * bvec[j];
+    sacc += __shfl_xor(sacc, 1, 64);
+    sacc += __shfl_xor(sacc, 2, 64);
+    if ((tid & 3) == 0) q += bvec[k0] * sacc;
+  }
+  q = block_sum(q, scratch);
+  if (tid == 0) st->guard_q = sqrt(q > 0.0 ? q : (q != q ? q : 0.0));
+}
+
+hipError_t launch_gram_verify(const double* G, int KP, int64_t K, float eps, const double* u,
+                              const double* alpha, const double* Dx, double* bvec, KState* st,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(gram_verify, dim3(1), dim3(1024), 0, s, G, KP, K, eps, u, alpha, Dx, bvec, st);
+  return hipGetLastError();
 }
 
 template <int KT>
@@ -244,24 +532,49 @@ static hipError_t launch_gram_kt(const float* X, int64_t K, int64_t d, int64_t l
 
 int gram_kt(int64_t K) { return K <= 32 ? 1 : K <= 64 ? 2 : K <= 128 ? 4 : K <= 256 ? 8 : 0; }
 
-size_t gram_slab_floats(int KT, int nb) { return (size_t)nb * (KT * (KT + 1) / 2) * 1024; }
+// block partials [nb][tiles][1024] fp32, then the reduction's fp64 tmp[kReduceGroups][n]
+size_t gram_slab_floats(int KT, int nb) {
+  return (size_t)(nb + 2 * kReduceGroups) * (KT * (KT + 1) / 2) * 1024;
+}
+
+template <int KT>
+static hipError_t launch_split_kt(const float* X, int64_t K, int64_t d, int64_t ldx,
+                                  const float* p, int nb, int64_t cpb, float* slab,
+                                  hipStream_t s) {
+  hipLaunchKernelGGL(gram_split_partial<KT>, dim3(nb), dim3(512), 0, s, X, K, d, ldx, p, cpb,
+                     slab);
+  return hipGetLastError();
+}
+
+int64_t gram_cols_per_block(int64_t d, int nb, bool split) {
+  const int64_t q = split ? kSplitBK : kGramJC;
+  return ((d + nb - 1) / nb + q - 1) / q * q;
+}
 
 hipError_t launch_gram(const float* X, int64_t K, int64_t d, int64_t ldx, const float* p, int nb,
-                       float* slab, double* G, hipStream_t s) {
+                       float* slab, double* G, hipStream_t s, bool split) {
   const int KT = gram_kt(K);
-  const int64_t cpb = ((d + nb - 1) / nb + kGramJC - 1) / kGramJC * kGramJC;
+  const int64_t cpb = gram_cols_per_block(d, nb, split);
   hipError_t e;
-  switch (KT) {
+  switch (KT * (split ? -1 : 1)) {
     case 1: e = launch_gram_kt<1>(X, K, d, ldx, p, nb, cpb, slab, s); break;
     case 2: e = launch_gram_kt<2>(X, K, d, ldx, p, nb, cpb, slab, s); break;
     case 4: e = launch_gram_kt<4>(X, K, d, ldx, p, nb, cpb, slab, s); break;
     case 8: e = launch_gram_kt<8>(X, K, d, ldx, p, nb, cpb, slab, s); break;
+    case -1: e = launch_split_kt<1>(X, K, d, ldx, p, nb, cpb, slab, s); break;
+    case -2: e = launch_split_kt<2>(X, K, d, ldx, p, nb, cpb, slab, s); break;
+    case -4: e = launch_split_kt<4>(X, K, d, ldx, p, nb, cpb, slab, s); break;
+    case -8: e = launch_split_kt<8>(X, K, d, ldx, p, nb, cpb, slab, s); break;
     default: return hipErrorInvalidValue;
   }
   if (e != hipSuccess) return e;
   const int64_t n = (int64_t)(KT * (KT + 1) / 2) * 1024;
-  hipLaunchKernelGGL(gram_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slab, nb, KT,
-                     G);
+  const int ng = std::min(kReduceGroups, nb);
+  double* tmp = reinterpret_cast<double*>(slab + (size_t)nb * n);
+  hipLaunchKernelGGL(gram_reduce_part, dim3((unsigned)((n + 255) / 256), ng), dim3(256), 0, s,
+                     slab, nb, n, tmp);
+  hipLaunchKernelGGL(gram_reduce_final, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tmp,
+                     ng, KT, G);
   return hipGetLastError();
 }
 

@@ -233,12 +233,12 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
     }
   }
 
-  if constexpr (SUM_ONLY) return;
-  // Per-block partials -> slab row.  [D2 (K)] [r (K), INIT only] [mv2] [gn2]
+  // Per-block partials -> slab row.  [D2 (K)] [r (K), INIT only] [mv2] [gn2];
+  // the Gram closing pass (SUM_ONLY) writes [||p - g||^2] [||g||^2] only.
   double* out = a.slab + (int64_t)blockIdx.x * a.slab_stride;
   const int i_c = row_of_lane<LPR, R>(c);
   constexpr int SPAN = R < LPR ? LPR / R : 1;   // lanes holding copies of one row sum
-  if ((c % SPAN) == 0) {
+  if (!SUM_ONLY && (c % SPAN) == 0) {
 #pragma unroll
     for (int m = 0; m < RPL; ++m) {
       const int64_t k = rg + (int64_t)NRG * (i_c + m);
@@ -261,7 +261,7 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
       m += s_fin[0][ww];
       g += s_fin[1][ww];
     }
-    const int64_t b = INIT ? 2 * K : K;
+    const int64_t b = SUM_ONLY ? 0 : INIT ? 2 * K : K;
     out[b] = m;
     out[b + 1] = g;
   }

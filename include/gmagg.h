@@ -56,8 +56,10 @@ enum gm_algo {
     GM_ALGO_AUTO = 0,
     GM_ALGO_STREAM = 1,       /* fused one-read-per-iteration streaming Weiszfeld */
     GM_ALGO_TWOPASS = 2,      /* two reads per iteration; any K */
-    GM_ALGO_GRAM = 3,         /* K x K Gram on MFMA, iterations in K-space (IDEAL only) */
-    GM_ALGO_RESIDENT = 4      /* small problems: X held in VGPRs, all iterations in one launch */
+    GM_ALGO_GRAM = 3,         /* K x K Gram on MFMA (bf16 h+m split, 4 products), iterations in
+                                 K-space (IDEAL only, K <= 256) */
+    GM_ALGO_RESIDENT = 4,     /* small problems: X held in VGPRs, all iterations in one launch */
+    GM_ALGO_GRAM_F32 = 5      /* the Gram on the exact f32-input MFMA (4x the issue cycles) */
 };
 
 /* Host-noise callback for GM_NOISE_HOST: fill the draws of Weiszfeld iteration

@@ -212,12 +212,13 @@ def test_gm2_large_fixed_point_property():
 
 # --- Gram-space variant (north_star's second design) ---------------------------
 
+@pytest.mark.parametrize("algo", ["gram", "gram_f32"])
 @pytest.mark.parametrize("name", golden_names("gm2"))
-def test_gram_matches_reference(name):
+def test_gram_matches_reference(name, algo):
     meta, arr = golden_case(name)
     K, d = arr["X"].shape
     o = _opts(meta, arr)
-    o["algo"] = "gram"
+    o["algo"] = algo
     X = torch.from_numpy(arr["X"].copy()).cuda()
     if meta["options"].get("maxiter", 200) == 0:
         assert bz().gm2(X, o) is o["guess"]
@@ -228,14 +229,15 @@ def test_gram_matches_reference(name):
         return
     out = bz().gm2(X, o)
     res = bz().aggregators.last_result
-    assert res.algo == "gram"
+    assert res.algo == algo
     assert rel_l2(out.cpu().numpy(), arr["out"]) <= TOL
     assert abs(res.iters - meta["iters"]) <= ITER_SLACK
 
 
+@pytest.mark.parametrize("algo", ["gram", "gram_f32"])
 @pytest.mark.parametrize("K", [1, 8, 32, 33, 64, 100, 128, 200, 256])
 @pytest.mark.parametrize("d", [4, 4096, 100_000])
-def test_gram_shapes_vs_oracle(K, d):
+def test_gram_shapes_vs_oracle(K, d, algo):
     g = torch.Generator().manual_seed(K * 31 + d)
     p = 0.07 * torch.randn(d, generator=g)
     X = p + 5e-4 * torch.randn(K, d, generator=g)
@@ -244,8 +246,8 @@ def test_gram_shapes_vs_oracle(K, d):
         X[K - B:] += 5e-3 * torch.randn(B, d, generator=g) + 2e-3
     opts = {"maxiter": 1000, "tol": 1e-5, "guess": p.clone()}
     want, tr = orc.gm2(X.clone(), dict(opts))
-    got = bz().gm2(X.cuda(), dict(opts, guess=p.cuda(), algo="gram"))
-    assert bz().aggregators.last_result.algo == "gram"
+    got = bz().gm2(X.cuda(), dict(opts, guess=p.cuda(), algo=algo))
+    assert bz().aggregators.last_result.algo == algo
     assert rel_l2(got.cpu().numpy(), want.numpy()) <= TOL
     assert abs(bz().aggregators.last_result.iters - tr.iters) <= max(ITER_SLACK, tr.iters // 10)
 
@@ -268,3 +270,62 @@ def test_gram_matches_stream_at_c4_scale():
     nb = m.aggregators.last_result.iters
     assert abs(na - nb) <= 1
     assert rel_l2(b.cpu().numpy(), a.cpu().numpy()) <= TOL
+
+
+def _c4_like(K, d, seed=20211):
+    m = bz()
+    X = torch.empty(K, d, device="cuda")
+    ctx = m.context()
+    s = torch.cuda.current_stream().cuda_stream
+    m._lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, X.data_ptr(), K, d, d, K // 5, 0.0, 0.05,
+                                             0.25, 0.5, seed, s), "fill")
+    g0 = torch.empty(d, device="cuda")
+    m._lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), d, 0.0, 0.01, seed + 1, s),
+                 "fill")
+    return X, g0
+
+
+def test_gram_split_vs_f32_and_auto_choice():
+    """The split-bf16 Gram agrees with the exact f32-MFMA Gram; AUTO keeps it (guard passes)."""
+    m = bz()
+    X, g0 = _c4_like(256, 1 << 20)
+    a = m.gm2(X, {"maxiter": 1000, "guess": g0, "algo": "gram_f32"})
+    na = m.aggregators.last_result.iters
+    b = m.gm2(X, {"maxiter": 1000, "guess": g0, "algo": "gram"})
+    nb = m.aggregators.last_result.iters
+    c = m.gm2(X, {"maxiter": 1000, "guess": g0})
+    assert m.aggregators.last_result.algo == "gram"
+    assert na == nb and abs(m.aggregators.last_result.iters - nb) == 0
+    assert rel_l2(b.cpu().numpy(), a.cpu().numpy()) <= 1e-6
+    assert rel_l2(c.cpu().numpy(), b.cpu().numpy()) == 0.0
+
+
+@pytest.mark.parametrize("case", ["far_offset", "tight_cluster", "g_error"])
+def test_gram_guard_falls_back_to_streaming(case):
+    """Data where the Gram may not reproduce the reference: the reference's fp32
+    movement floor ~2^-24 ||g|| exceeds tol/3 (AUTO must run the streaming path),
+    or D_k ~ 1e-7 G_kk (the a-posteriori check decides; either way the result
+    must match the oracle)."""
+    m = bz()
+    g = torch.Generator().manual_seed(11)
+    K, d = 64, 1 << 18
+    if case == "far_offset":
+        X = 3.0 + 0.05 * torch.randn(K, d, generator=g)
+        p = torch.zeros(d)
+    elif case == "tight_cluster":
+        X = 1.0 + 1e-3 * torch.randn(K, d, generator=g)
+        X[50:] += 0.05
+        p = torch.zeros(d)
+    else:            # ||g|| small enough for the floor test; D_k ~ 1e-7 G_kk
+        X = 0.05 + 1e-5 * torch.randn(K, d, generator=g)
+        p = torch.zeros(d)
+    opts = {"maxiter": 30, "tol": 1e-5, "guess": p}
+    want, tr = orc.gm2(X.clone(), dict(opts))
+    got = m.gm2(X.cuda(), dict(opts, guess=p.cuda()))
+    res = m.aggregators.last_result
+    if case != "g_error":            # the floor test alone decides these
+        assert res.algo == "stream"
+    # whichever path AUTO kept, it reproduces the reference
+    assert rel_l2(got.cpu().numpy(), want.numpy()) <= TOL
+    if res.converged and tr.iters < 30:
+        assert abs(res.iters - tr.iters) <= ITER_SLACK
