@@ -183,6 +183,16 @@ bool pick_cfg(int64_t K, int V, int64_t ldx, PassCfg* cfg) {
   return pass_cfg_supported(*cfg);
 }
 
+// Tile of the passes without phase A's weighted sum feeding phase B (INIT) or
+// without phase B (the Gram closing pass): at 128 < K <= 256 the 1-KiB row
+// segments of (16,64,16) beat the STEP tile (16,32,8): 2.81 / 2.76 vs 3.00 /
+// 2.99 ms at K=256 x d=15.6M (profiles/r02_sweep_close.txt).
+PassCfg light_cfg(int64_t K, const PassCfg& step) {
+  if (getenv("GMAGG_PASS_CFG") || step.V != 4 || K <= 128 || K > 256) return step;
+  const PassCfg c{4, 16, 64, 16, 1};
+  return pass_cfg_supported(c) ? c : step;
+}
+
 int pick_vec(const float* X, int64_t d, int64_t ldx) {
   const uintptr_t p = reinterpret_cast<uintptr_t>(X);
   if (d % 4 == 0 && ldx % 4 == 0 && p % 16 == 0) return 4;
@@ -284,9 +294,13 @@ int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const
   }
   const int64_t cpb = gram_cols_per_block(d, nb_g, split);
   nb_g = (int)std::max<int64_t>(1, (d + cpb - 1) / cpb);
-  const int J = cfg.LPR * cfg.V;
+  // closing pass: the STEP tile when it also yields the distances (guarded), else
+  // the lighter sum-only tile
+  const PassCfg ccfg = guarded ? cfg : light_cfg(K, cfg);
+  const int J = ccfg.LPR * ccfg.V;
   const int nb_p = (int)std::max<int64_t>(
-      1, std::min<int64_t>((d + J - 1) / J, (int64_t)c->num_cu * pass_blocks_per_cu(cfg, 3)));
+      1, std::min<int64_t>((d + J - 1) / J,
+                           (int64_t)c->num_cu * pass_blocks_per_cu(ccfg, guarded ? 0 : 3)));
   Workspace w;
   int rc = ensure_ws(c, K, d, nb_p, &w, gram_slab_floats(KT, nb_g), KP);
   if (rc) return rc;
@@ -314,7 +328,7 @@ int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const
   a.X = X; a.K = K; a.d = d; a.ldx = ldx;
   a.g_old = p; a.g_new = out; a.coef = w.coef; a.st = w.st;
   a.slab = w.slab; a.slab_stride = S;
-  HIPCHK(launch_pass(cfg, guarded ? 0 : 3, nb_p, a, s));
+  HIPCHK(launch_pass(ccfg, guarded ? 0 : 3, nb_p, a, s));
   HIPCHK(launch_slab_reduce(w.slab, nb_p, S, w.sums, w.st, s));   // [D (K)] [||p-g||^2, ||g||^2]
   rc = allreduce(c, w.sums, S, s);
   if (rc) return rc;
@@ -513,13 +527,14 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   const int init_mode = o->mode == GM_MODE_AIRCOMP ? 2 : 1;   // ||x_k||^2 only for AirComp
 
   int nb_step, nb_init;
+  const PassCfg cfg_i = light_cfg(K, cfg);
   if (algo == GM_ALGO_STREAM) {
-    const int J = cfg.LPR * cfg.V;
-    const int64_t nch = (d + J - 1) / J;
+    const int J = cfg.LPR * cfg.V, Ji = cfg_i.LPR * cfg_i.V;
+    const int64_t nch = (d + J - 1) / J, nchi = (d + Ji - 1) / Ji;
     const int64_t cap_s = (int64_t)c->num_cu * pass_blocks_per_cu(cfg, 0);
-    const int64_t cap_i = (int64_t)c->num_cu * pass_blocks_per_cu(cfg, init_mode);
+    const int64_t cap_i = (int64_t)c->num_cu * pass_blocks_per_cu(cfg_i, init_mode);
     nb_step = (int)std::max<int64_t>(1, std::min(nch, cap_s));
-    nb_init = (int)std::max<int64_t>(1, std::min(nch, cap_i));
+    nb_init = (int)std::max<int64_t>(1, std::min(nchi, cap_i));
   } else {
     nb_step = nb_init = twopass_blocks(K, d, c->num_cu);
   }
@@ -592,7 +607,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       a.g_old = g_old; a.g_new = g_new; a.coef = w.coef; a.st = w.st;
       a.slab = w.slab; a.slab_stride = S;
       a.noise = noise_kind; a.hnoise = w.hnoise; a.seed = o->seed; a.iter = t; a.col_off = col_off;
-      HIPCHK(launch_pass(cfg, init ? init_mode : 0, init ? nb_init : nb_step, a, s));
+      HIPCHK(launch_pass(init ? cfg_i : cfg, init ? init_mode : 0, init ? nb_init : nb_step, a, s));
       if (!init) { rc2 = record_pass_end(c, s, e0, e1); if (rc2) return rc2; }
       HIPCHK(launch_slab_reduce(w.slab, init ? nb_init : nb_step, S, w.sums, w.st, s));
     } else {
@@ -618,16 +633,18 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   // Polling every iteration (large passes): read iteration t-1's state while
   // iteration t is already queued, so the device never waits for the host.  If
   // t-1 stopped the loop, iteration t's launches see `done` and exit at once.
-  const bool lagged = check_every == 1 && !host_noise;
+  static const bool no_lag = getenv("GMAGG_NO_LAG") != nullptr;   // A/B switch
+  const bool lagged = check_every == 1 && !host_noise && !no_lag;
   if (lagged)
     for (auto& e : c->poll_ev)
       if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   int64_t pending = -1;   // iteration whose KState copy is in flight (lagged)
 
-  int64_t t = 0;
+  int64_t t = 0, enqueued = 0;
   for (; t < o->maxiter; ++t) {
     rc = do_pass(t);
     if (rc) return rc;
+    enqueued = t + 1;
     const bool last = t + 1 == o->maxiter;
     ka.t = t;
     if (host_noise) {
@@ -671,6 +688,12 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   r.converged = hst->converged;
   r.algo_used = algo;
   if (r.iters < 1) return fail(GM_ERR_HIP, "Weiszfeld loop recorded no iteration");
+  // passes queued after the stop (lagged poll) exited at once: not timed as passes
+  for (int64_t k = r.iters; k < enqueued && c->timing && !c->ev_used.empty(); ++k) {
+    c->ev_free.push_back(c->ev_used.back().first);
+    c->ev_free.push_back(c->ev_used.back().second);
+    c->ev_used.pop_back();
+  }
   HIPCHK(hipMemcpyAsync(out, w.g[(r.iters - 1) & 1], sizeof(float) * d, hipMemcpyDeviceToDevice, s));
   if (res) *res = r;
   return GM_OK;

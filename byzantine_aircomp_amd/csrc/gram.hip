@@ -254,13 +254,17 @@ struct SplitProducer {
   }
 };
 
-template <int KT>
+template <int KT, int DBG>
 __device__ __forceinline__ void split_producer(const float* __restrict__ X, int64_t K,
                                                int64_t ldx, const float* __restrict__ p,
                                                int64_t c_begin, int64_t c_end, int nstage,
                                                __bf16 (*lds)[2][GramShape<KT>::KP * kSplitLS]) {
   SplitProducer<KT> P;
   const int t = threadIdx.x - 256;
+  if constexpr (DBG == 2) {          // timing probe: no global loads
+    for (int s = 0; s <= nstage; ++s) __syncthreads();
+    return;
+  }
   P.X = X; P.p = p; P.K = K; P.ldx = ldx; P.c_begin = c_begin; P.c_end = c_end;
   P.r0 = t >> 4; P.cg = t & 15;
   P.lrow = (uint32_t)P.r0 * (uint32_t)ldx;
@@ -286,12 +290,12 @@ __device__ __forceinline__ void split_producer(const float* __restrict__ X, int6
 // Consumer wave W (W < 0: idle slot for KT < 8): per 16-column step it reads the
 // h/m fragments of row tiles W..KT-1 once (one ds_read_b128 each) and issues 4
 // MFMAs per tile, all registers statically indexed.
-template <int KT, int W>
+template <int KT, int W, int DBG>
 __device__ __forceinline__ void split_consumer(int nstage, float* __restrict__ slab,
                                                __bf16 (*lds)[2][GramShape<KT>::KP * kSplitLS]) {
   using Sh = GramShape<KT>;
   constexpr int NT = Sh::PER_WAVE;
-  constexpr bool MMA = W >= 0;
+  constexpr bool MMA = W >= 0 && DBG != 1;    // DBG 1: timing probe without MFMAs
   constexpr int LO = KT == 1 ? 0 : (W < 0 ? 0 : W);
   const int lane = threadIdx.x & 63;
   f32x16 acc[NT];
@@ -331,7 +335,7 @@ __device__ __forceinline__ void split_consumer(int nstage, float* __restrict__ s
   }
 }
 
-template <int KT>
+template <int KT, int DBG = 0>
 __global__ void __launch_bounds__(512, 1) gram_split_partial(const float* __restrict__ X,
                                                              int64_t K, int64_t d, int64_t ldx,
                                                              const float* __restrict__ p,
@@ -343,25 +347,25 @@ __global__ void __launch_bounds__(512, 1) gram_split_partial(const float* __rest
   const int64_t c_end = c_begin + cols_per_block < d ? c_begin + cols_per_block : d;
   const int nstage = c_begin < c_end ? (int)((c_end - c_begin + kSplitBK - 1) / kSplitBK) : 0;
   if (w >= 4) {
-    split_producer<KT>(X, K, ldx, p, c_begin, c_end, nstage, lds);
+    split_producer<KT, DBG>(X, K, ldx, p, c_begin, c_end, nstage, lds);
     return;
   }
   if constexpr (KT == 8) {
     switch (w) {
-      case 0: split_consumer<KT, 0>(nstage, slab, lds); break;
-      case 1: split_consumer<KT, 1>(nstage, slab, lds); break;
-      case 2: split_consumer<KT, 2>(nstage, slab, lds); break;
-      default: split_consumer<KT, 3>(nstage, slab, lds); break;
+      case 0: split_consumer<KT, 0, DBG>(nstage, slab, lds); break;
+      case 1: split_consumer<KT, 1, DBG>(nstage, slab, lds); break;
+      case 2: split_consumer<KT, 2, DBG>(nstage, slab, lds); break;
+      default: split_consumer<KT, 3, DBG>(nstage, slab, lds); break;
     }
   } else if constexpr (KT == 4) {
     switch (w) {
-      case 0: split_consumer<KT, 0>(nstage, slab, lds); break;
-      case 1: split_consumer<KT, 1>(nstage, slab, lds); break;
-      default: split_consumer<KT, -1>(nstage, slab, lds); break;
+      case 0: split_consumer<KT, 0, DBG>(nstage, slab, lds); break;
+      case 1: split_consumer<KT, 1, DBG>(nstage, slab, lds); break;
+      default: split_consumer<KT, -1, DBG>(nstage, slab, lds); break;
     }
   } else {
-    if (w == 0) split_consumer<KT, 0>(nstage, slab, lds);
-    else split_consumer<KT, -1>(nstage, slab, lds);
+    if (w == 0) split_consumer<KT, 0, DBG>(nstage, slab, lds);
+    else split_consumer<KT, -1, DBG>(nstage, slab, lds);
   }
 }
 
@@ -541,8 +545,17 @@ template <int KT>
 static hipError_t launch_split_kt(const float* X, int64_t K, int64_t d, int64_t ldx,
                                   const float* p, int nb, int64_t cpb, float* slab,
                                   hipStream_t s) {
-  hipLaunchKernelGGL(gram_split_partial<KT>, dim3(nb), dim3(512), 0, s, X, K, d, ldx, p, cpb,
-                     slab);
+  // GMAGG_GRAM_DEBUG = 1 / 2: timing probes without MFMAs / without loads (wrong G)
+  static const int dbg = [] { const char* e = getenv("GMAGG_GRAM_DEBUG"); return e ? atoi(e) : 0; }();
+  if (dbg == 1)
+    hipLaunchKernelGGL((gram_split_partial<KT, 1>), dim3(nb), dim3(512), 0, s, X, K, d, ldx, p, cpb,
+                       slab);
+  else if (dbg == 2)
+    hipLaunchKernelGGL((gram_split_partial<KT, 2>), dim3(nb), dim3(512), 0, s, X, K, d, ldx, p, cpb,
+                       slab);
+  else
+    hipLaunchKernelGGL((gram_split_partial<KT, 0>), dim3(nb), dim3(512), 0, s, X, K, d, ldx, p, cpb,
+                       slab);
   return hipGetLastError();
 }
 

