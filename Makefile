@@ -26,3 +26,15 @@ clean:
 	rm -rf $(BUILD) $(LIB)
 
 .PHONY: all clean
+
+# A/B build: the streaming pass with buffer_load + one shared VGPR offset
+# (GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so selects it at run time).
+ALT := byzantine_aircomp_amd/libgmagg_alt.so
+$(BUILD)/alt/stream_pass.o: $(CSRC)/stream_pass.hip $(HDRS)
+	@mkdir -p $(BUILD)/alt
+	$(HIPCC) $(HIPFLAGS) -DGMK_BUFFER_LOADS -c $< -o $@
+$(ALT): $(BUILD)/alt/stream_pass.o $(filter-out $(BUILD)/stream_pass.o,$(OBJS))
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl \
+	    -Wl,-rpath,/opt/rocm/lib
+alt: $(ALT)
+.PHONY: alt

@@ -178,7 +178,7 @@ bool pick_cfg(int64_t K, int V, int64_t ldx, PassCfg* cfg) {
     }
   }
   // lane offsets are 32-bit: (rows per wave - 1) * ldx + ldx must fit in bytes
-  if ((uint64_t)(64 / lpr) * (uint64_t)ldx * 4u >= (1ull << 32)) return false;
+  if ((uint64_t)(64 / lpr) * (uint64_t)ldx * 4u >= (1ull << 31)) return false;   // buffer offsets
   *cfg = PassCfg{V, nw, lpr, r, occ};
   return pass_cfg_supported(*cfg);
 }

@@ -24,6 +24,28 @@ __device__ __forceinline__ void load_cols(const float* __restrict__ p, float (&o
   }
 }
 
+// V consecutive floats at byte offset `off` from the wave-uniform `base`, through
+// a raw buffer resource (num_records 2^31: offsets >= 0x80000000 read 0),
+// streamed (slc).  One VGPR of address per load instead of a 64-bit pointer.
+template <int V>
+__device__ __forceinline__ void load_rows(const float* base, uint32_t off, float (&o)[V]) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x80000000, 0x00020000);
+  if constexpr (V == 4) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const f4 v = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = v[i];
+  } else if constexpr (V == 2) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 v = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 2));
+    o[0] = v[0];
+    o[1] = v[1];
+  } else {
+    o[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 2));
+  }
+}
+
 template <int A, int B> struct cmin { static constexpr int v = A < B ? A : B; };
 template <int N> struct ilog2 { static constexpr int v = 1 + ilog2<N / 2>::v; };
 template <> struct ilog2<1> { static constexpr int v = 0; };

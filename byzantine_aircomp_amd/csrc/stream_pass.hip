@@ -75,15 +75,27 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
   const int64_t nch = (d + J - 1) / J;
   const int64_t grid = gridDim.x;
 
-  // Row r of this thread = wave-uniform base (SGPR pair) + 32-bit lane offset.
-  const float* base[R];
+  // Row r of this thread = wave-uniform row-group base (a buffer resource in
+  // SGPRs, rebuilt per chunk by scalar adds) + ONE 32-bit lane byte offset shared
+  // by all R rows.  Rows >= K and columns >= d get an out-of-range offset: the
+  // buffer unit returns 0 for them, so every load is unconditional and no
+  // per-row 64-bit address is kept in VGPRs.
+  // Rows: SGPR base + lane offset through global_load (measured 1.8 % faster than
+  // buffer_load with one shared VGPR offset, -DGMK_BUFFER_LOADS, on the C3 pass:
+  // 6.90 vs 7.03 ms, same box; profiles/r02_ab_loads.txt).
   bool rval[R];
 #pragma unroll
-  for (int i = 0; i < R; ++i) {
-    base[i] = a.X + (int64_t)(w * QW + NRG * i) * a.ldx;
-    rval[i] = rg + (int64_t)NRG * i < K;
-  }
-  const uint32_t loff = (uint32_t)q * (uint32_t)a.ldx;
+  for (int i = 0; i < R; ++i) rval[i] = rg + (int64_t)NRG * i < K;
+#ifndef GMK_BUFFER_LOADS
+  const float* base[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) base[i] = a.X + (int64_t)(w * QW + NRG * i) * a.ldx;
+  const uint32_t goff = (uint32_t)q * (uint32_t)a.ldx;
+#else
+  const uint32_t loff = ((uint32_t)q * (uint32_t)a.ldx + (uint32_t)(c * V)) * 4u;
+  const int64_t row_step = (int64_t)NRG * a.ldx;   // elements between row groups i, i+1
+  const float* wbase = a.X + (int64_t)(w * QW) * a.ldx;
+#endif
 
   float wt[OCC > 1 ? 1 : R];
   float a_noise = 0.f;
@@ -101,7 +113,8 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
   auto fetch = [&](int64_t ch, T& t) {
     const int64_t col = ch * J + (int64_t)c * V;
     const bool cval = ch < nch && col < d;   // V | d: a lane's group is all-in or all-out
-    const uint32_t off = loff + (uint32_t)col;
+#ifndef GMK_BUFFER_LOADS
+    const uint32_t off = goff + (uint32_t)col;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       if (cval && rval[i]) {
@@ -111,6 +124,14 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
         for (int v = 0; v < V; ++v) t.x[i][v] = 0.f;
       }
     }
+#else
+    const float* cb = wbase + (ch < nch ? ch * J : 0);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const uint32_t off = (cval && rval[i]) ? loff : 0x80000000u;   // OOB reads 0
+      load_rows<V>(cb + i * row_step, off, t.x[i]);
+    }
+#endif
     if constexpr (INIT) {
 #pragma unroll
       for (int v = 0; v < V; ++v) t.g[v] = cval ? a.g_old[col + v] : 0.f;
