@@ -26,7 +26,7 @@ def _problem(K, d, B, seed):
     return X.cuda(), p.cuda()
 
 
-def _sharded(X, p, P, opts, aircomp):
+def _sharded(X, p, P, opts, aircomp, check_every=0, algo=0):
     from byzantine_aircomp_amd import _lib
     from byzantine_aircomp_amd.aggregators import Context
     from byzantine_aircomp_amd.sharded import _wrap, shard_range
@@ -60,6 +60,7 @@ def _sharded(X, p, P, opts, aircomp):
             o = _lib.GmOpts()
             o.maxiter, o.tol, o.eps = opts["maxiter"], opts["tol"], 1e-4
             o.mode = _lib.GM_MODE_AIRCOMP if aircomp else _lib.GM_MODE_IDEAL
+            o.check_every, o.algo = check_every, algo
             if aircomp:
                 o.has_noise, o.noise_var, o.P_max, o.seed = 1, opts["noise_var"], 1.0, opts["seed"]
             rr = _lib.GmResult()
@@ -67,7 +68,7 @@ def _sharded(X, p, P, opts, aircomp):
                                                 g0.data_ptr(), res.data_ptr(), C.byref(o),
                                                 C.byref(rr), None), "sharded gm")
             torch.cuda.synchronize(dev)
-            out[r] = (lo, hi, res, rr.iters)
+            out[r] = (lo, hi, res, rr.iters, rr.algo_used)
         except Exception as e:  # noqa: BLE001
             errs.append(e)
             barrier.abort()
@@ -80,7 +81,8 @@ def _sharded(X, p, P, opts, aircomp):
     assert not errs, errs
     full = torch.empty(d, device=dev)
     iters = {o_[3] for o_ in out}
-    for lo, hi, res, _ in out:
+    _sharded.algos = {o_[4] for o_ in out}
+    for lo, hi, res, _, _ in out:
         full[lo:hi] = res
     return full, iters
 
@@ -127,3 +129,37 @@ def test_rccl_single_rank_path():
                                         out.data_ptr(), C.byref(o), C.byref(rr), None), "rccl gm2")
     torch.cuda.synchronize()
     assert rel_l2(out.cpu().numpy(), want.cpu().numpy()) <= 1e-7
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_sharded_lagged_poll_equals_unsharded(P):
+    """check_every = 1: every rank reads iteration t-1's state while t is queued
+    (the large-problem host loop); all ranks must stop together."""
+    import byzantine_aircomp_amd as bz
+    X, p = _problem(200, 50_000, 40, seed=10 + P)
+    opts = {"maxiter": 1000, "tol": 1e-5}
+    want = bz.gm2(X, dict(opts, guess=p, check_every=1))
+    n = bz.aggregators.last_result.iters
+    got, iters = _sharded(X, p, P, opts, aircomp=False, check_every=1)
+    assert len(iters) == 1 and abs(iters.pop() - n) <= 1
+    assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-6
+
+
+@pytest.mark.parametrize("algo", [0, 3])          # AUTO (guarded Gram) and explicit split Gram
+def test_sharded_gram_equals_unsharded(algo):
+    """d-sharded Gram: one all-reduce of G (and of the closing pass's sums for the
+    guard); every rank takes the same guard decision."""
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd import _lib
+    K, P = 64, 2
+    d = 2 * (1 << 18) + 4096
+    X, p = _problem(K, d, 12, seed=21)
+    opts = {"maxiter": 1000, "tol": 1e-5}
+    want = bz.gm2(X, dict(opts, guess=p, algo="stream"))
+    n = bz.aggregators.last_result.iters
+    got, iters = _sharded(X, p, P, opts, aircomp=False, algo=algo)
+    assert len(iters) == 1 and abs(iters.pop() - n) <= 1
+    assert len(_sharded.algos) == 1
+    if algo == 3:
+        assert _sharded.algos == {_lib.GM_ALGO_GRAM}
+    assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-5
