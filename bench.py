@@ -234,9 +234,11 @@ def main():
             dc = min(args.cpu_d, d)
             line["cpu_baseline"] = cpu_baseline(X[:, :dc].contiguous(), g0[:dc], res.iters, d_total)
         print(json.dumps(line), flush=True)
+    del out
+    torch.cuda.synchronize(dev)
+    ctx.close()                       # RCCL communicator + workspace, before the process group
     if world > 1:
         torch.distributed.destroy_process_group()
-    del out
 
 
 if __name__ == "__main__":

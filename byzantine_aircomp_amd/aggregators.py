@@ -97,6 +97,17 @@ class Context:
                                                C.byref(n)), "gm_ctx_pass_timing")
         return ms.value, n.value
 
+    def close(self):
+        """Destroy the context now (workspace, RCCL communicator); idempotent.
+        Multi-process callers close before torch.distributed.destroy_process_group()
+        rather than leaving the communicator to interpreter teardown."""
+        h, self.handle = getattr(self, "handle", None), None
+        if h:
+            self.lib.gm_ctx_destroy(h)
+        for k, v in list(_contexts.items()):
+            if v is self:
+                del _contexts[k]
+
     def __del__(self):
         try:
             if getattr(self, "handle", None):

@@ -145,3 +145,8 @@ class ShardedGM:
 
     def gm(self, X, options=None):
         return self._run(X, options or {}, aircomp=True)
+
+    def close(self):
+        """Release this rank's context and RCCL communicator (call before
+        torch.distributed.destroy_process_group())."""
+        self.ctx.close()
