@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--maxiter", type=int, default=1000)
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-d", type=int, default=2_000_000, help="CPU sample width")
+    p.add_argument("--dist", action="store_true",
+                   help="take the multi-rank path (process group, RCCL comm, d-shard) even at "
+                        "world size 1: a one-GPU rehearsal of the N>1 code")
     return p.parse_args()
 
 
@@ -108,11 +111,17 @@ def cpu_baseline(X, g0, iters, d_full):
 
 def main():
     args = parse()
+    # stdout carries exactly one JSON line: everything else written to fd 1 (RCCL's
+    # init banner, library chatter) is sent to stderr; the line goes to the saved fd.
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dist_path = world > 1 or args.dist
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     import byzantine_aircomp_amd as bz
@@ -122,8 +131,11 @@ def main():
     lo, hi = shard_range(d_total, world, rank)
     d = hi - lo
     ctx = bz.context(dev)
-    if world > 1:
+    if dist_path:
         import torch.distributed as dist
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29533"), ("RANK", "0"),
+                     ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)      # plain `python bench.py --dist` (rehearsal)
         dist.init_process_group("nccl", device_id=dev)
         ctx.set_shard(d_total, lo)
         uid = [None]
@@ -153,7 +165,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_path:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     ctx.pass_timing(True)
@@ -161,13 +173,13 @@ def main():
     for _ in range(args.steps):
         out = step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_path:
         torch.distributed.barrier()
     t1 = time.perf_counter()
     pass_ms, launches = ctx.pass_timing(False)
     res = bz.aggregators.last_result
     elapsed = t1 - t0
-    if world > 1:
+    if dist_path:
         t = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -225,7 +237,7 @@ def main():
                                    f"Byzantine, tol 1e-5, maxiter {args.maxiter}"
                                    + (f", noise_var {args.var}" if args.agg == "gm" else ""),
                        "K": K, "d": d_total, "byzantine": B, "iters": res.iters,
-                       "algo": res.algo, "parallelism": f"d-shard x{world}" if world > 1 else "none",
+                       "algo": res.algo, "parallelism": f"d-shard x{world}" if dist_path else "none",
                        "passes_per_aggregation": 2 if res.algo.startswith("gram") else res.iters + 1},
             "roofline": roof,
             "cpu_baseline": None,
@@ -233,11 +245,11 @@ def main():
         if world == 1 and not args.no_cpu and args.agg == "gm2":
             dc = min(args.cpu_d, d)
             line["cpu_baseline"] = cpu_baseline(X[:, :dc].contiguous(), g0[:dc], res.iters, d_total)
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     del out
     torch.cuda.synchronize(dev)
     ctx.close()                       # RCCL communicator + workspace, before the process group
-    if world > 1:
+    if dist_path:
         torch.distributed.destroy_process_group()
 
 
