@@ -6,7 +6,7 @@ ARCH     ?= gfx950
 CSRC     := byzantine_aircomp_amd/csrc
 BUILD    := build/obj
 LIB      := byzantine_aircomp_amd/libgmagg.so
-HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-result -DGMK_PIPE_VARIANT \
+HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-result \
             -I include -munsafe-fp-atomics
 SRCS     := $(CSRC)/stream_pass.hip $(CSRC)/gram.hip $(CSRC)/resident.hip $(CSRC)/coordinate.hip $(CSRC)/weiszfeld.hip $(CSRC)/oma.hip $(CSRC)/api.hip
 OBJS     := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(SRCS))
@@ -27,12 +27,13 @@ clean:
 
 .PHONY: all clean
 
-# A/B build: the streaming pass with buffer_load + one shared VGPR offset
-# (GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so selects it at run time).
+# A/B build: the streaming pass with the two-tile PIPE schedule compiled in
+# (GMAGG_PASS_VARIANT=1 selects it; GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so
+# loads this library at run time).
 ALT := byzantine_aircomp_amd/libgmagg_alt.so
 $(BUILD)/alt/stream_pass.o: $(CSRC)/stream_pass.hip $(HDRS)
 	@mkdir -p $(BUILD)/alt
-	$(HIPCC) $(HIPFLAGS) -DGMK_BUFFER_LOADS -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DGMK_PIPE_VARIANT -c $< -o $@
 $(ALT): $(BUILD)/alt/stream_pass.o $(filter-out $(BUILD)/stream_pass.o,$(OBJS))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl \
 	    -Wl,-rpath,/opt/rocm/lib

@@ -57,6 +57,9 @@ def parse():
     p.add_argument("--agg", default="gm2", choices=["gm2", "gm"])
     p.add_argument("--var", type=float, default=None, help="gm noise variance (None = no AWGN)")
     p.add_argument("--maxiter", type=int, default=1000)
+    p.add_argument("--layout", default="rows", choices=["rows", "panels"],
+                   help="client matrix layout: rows = the reference's [K, d] stack; panels = "
+                        "ClientPanels [ceil(d/W)][K][W] (streaming algorithm)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-d", type=int, default=2_000_000, help="CPU sample width")
     p.add_argument("--dist", action="store_true",
@@ -158,9 +161,12 @@ def main():
     if args.agg == "gm":
         opts.update(noise_var=args.var, seed=2021)
     agg = bz.gm2 if args.agg == "gm2" else bz.gm
+    Xin = X
+    if args.layout == "panels":
+        Xin = bz.ClientPanels.from_rows(X)      # same values, panel layout (packed once)
 
     def step():
-        return agg(X, opts)
+        return agg(Xin, opts)
 
     for _ in range(args.warmup):
         step()
@@ -237,7 +243,7 @@ def main():
                                    f"Byzantine, tol 1e-5, maxiter {args.maxiter}"
                                    + (f", noise_var {args.var}" if args.agg == "gm" else ""),
                        "K": K, "d": d_total, "byzantine": B, "iters": res.iters,
-                       "algo": res.algo, "parallelism": f"d-shard x{world}" if dist_path else "none",
+                       "algo": res.algo, "layout": args.layout, "parallelism": f"d-shard x{world}" if dist_path else "none",
                        "passes_per_aggregation": 2 if res.algo.startswith("gram") else res.iters + 1},
             "roofline": roof,
             "cpu_baseline": None,

@@ -10,5 +10,6 @@ reference's training loop.
 """
 from .aggregators import (GMResult, Krum, OMA, context, gm, gm2, mean, median,  # noqa: F401
                           trimmed_mean)
+from .panels import ClientPanels, panel_width  # noqa: F401
 
 __version__ = "0.1.0"

@@ -18,6 +18,7 @@ GM_MODE_IDEAL, GM_MODE_AIRCOMP = 0, 1
 GM_NOISE_PHILOX, GM_NOISE_HOST = 0, 1
 GM_ALGO_AUTO, GM_ALGO_STREAM, GM_ALGO_TWOPASS, GM_ALGO_GRAM, GM_ALGO_RESIDENT = 0, 1, 2, 3, 4
 GM_ALGO_GRAM_F32 = 5
+GM_LAYOUT_ROWS, GM_LAYOUT_PANELS = 0, 1
 
 NOISE_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.POINTER(C.c_float),
                        C.POINTER(C.c_float), C.POINTER(C.c_float))
@@ -39,7 +40,7 @@ class GmOpts(C.Structure):
         ("noise_cb", NOISE_CB),
         ("noise_user", C.c_void_p),
         ("check_every", C.c_int32),
-        ("reserved", C.c_int32),
+        ("layout", C.c_int32),
     ]
 
 
@@ -64,6 +65,7 @@ SIGNATURES = [
     ("gm_ctx_init_rccl", C.c_int, [_P, _P, C.c_int, C.c_int]),
     ("gm_weiszfeld_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _P, _P, C.POINTER(GmOpts),
                                    C.POINTER(GmResult), _P]),
+    ("gm_panel_width", _I64, [_I64]),
     ("gm_weiszfeld_batched_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P,
                                            _I64, C.POINTER(GmOpts), C.POINTER(GmResult), _P]),
     ("gm_mean_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _P, _P]),

@@ -25,7 +25,10 @@ Extensions (ignored by the reference's loop): options ``noise_source``
 (``"device"``: on-device Philox, the default; ``"host"``: the reference's own
 ``torch.normal`` draws on the CPU generator, in its order, for exact
 comparison), ``seed`` (Philox key; drawn from the torch CPU generator when
-absent) and ``algo`` (``"auto"``, ``"stream"``, ``"twopass"``).  The trace of
+absent) and ``algo`` (``"auto"``, ``"stream"``, ``"twopass"``, ``"gram"``,
+``"gram_f32"``, ``"resident"``).  ``gm2`` / ``gm`` also accept a
+``ClientPanels`` (panels.py: the same K x d values in the panel layout the
+streaming pass reads as contiguous blocks) in place of the ``[K, d]`` tensor.  The trace of
 the last call (iterations, last movement) is in ``last_result``.
 
 There is no CPU path: without a GPU or without libgmagg.so these raise.
@@ -40,6 +43,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
+from .panels import ClientPanels
 
 __all__ = ["gm2", "gm", "OMA", "mean", "median", "trimmed_mean", "Krum", "GMResult",
            "last_result", "Context", "context"]
@@ -202,9 +206,14 @@ def _weiszfeld(wList: torch.Tensor, options: dict, aircomp: bool):
     if maxiter <= 0:                        # M:145 / M:173 loop body never runs
         last_result = GMResult(0, float("nan"), False, "none")
         return guess
-    X = _stage(wList)
-    X, ldx = _rows(X)
-    K, d = X.shape
+    layout = _lib.GM_LAYOUT_ROWS
+    if isinstance(wList, ClientPanels):
+        X, ldx, layout = wList.data, wList.panel_stride, _lib.GM_LAYOUT_PANELS
+        K, d = wList.shape
+    else:
+        X = _stage(wList)
+        X, ldx = _rows(X)
+        K, d = X.shape
     g0 = guess.detach().to(device=X.device, dtype=torch.float32).contiguous()
     if g0.numel() != d:
         raise ValueError(f"guess has {g0.numel()} elements, wList rows have {d}")
@@ -220,6 +229,7 @@ def _weiszfeld(wList: torch.Tensor, options: dict, aircomp: bool):
     o.mode = _lib.GM_MODE_AIRCOMP if aircomp else _lib.GM_MODE_IDEAL
     o.algo = _ALGOS[opts.get("algo", "auto")]
     o.check_every = int(opts.get("check_every", 0))
+    o.layout = layout
     cb = None
     if aircomp:
         var = opts["noise_var"]

@@ -366,6 +366,11 @@ extern "C" {
 const char* gm_last_error(void) { return g_err.c_str(); }
 int gm_abi_version(void) { return GMAGG_ABI_VERSION; }
 
+int64_t gm_panel_width(int64_t K) {
+  PassCfg cfg{};
+  return K >= 1 && pick_cfg(K, 4, 1, &cfg) ? (int64_t)cfg.LPR * cfg.V : 0;
+}
+
 int gm_ctx_create(int device, gm_ctx** out) {
   if (!out) return fail(GM_ERR_INVALID, "gm_ctx_create: out is NULL");
   *out = nullptr;
@@ -482,7 +487,24 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   // Algorithm and tile.
   PassCfg cfg{};
   int algo = o->algo;
-  const int V = pick_vec(X, d, ldx);
+  const bool panels = o->layout == GM_LAYOUT_PANELS;
+  if (o->layout != GM_LAYOUT_ROWS && !panels)
+    return fail(GM_ERR_INVALID, "gm_weiszfeld_f32: unknown layout %d", o->layout);
+  if (panels) {
+    // [ceil(d/W)][K][W] panels: the streaming pass only, with the tile whose chunk
+    // width is W (pick_cfg's tile for K; light_cfg's wider INIT tile is not used).
+    const int64_t W = gm_panel_width(K);
+    if (W == 0 || !pick_cfg(K, 4, W, &cfg) || cfg.LPR * cfg.V != W)
+      return fail(GM_ERR_UNSUPPORTED, "panel layout: no streaming tile of width %lld for K=%lld",
+                  (long long)W, (long long)K);
+    if (ldx < K * W || (reinterpret_cast<uintptr_t>(X) & 15) || K * W * 4 > 0x7fffffff)
+      return fail(GM_ERR_INVALID, "panel layout: need panel stride >= K*W (%lld), 16-byte aligned "
+                  "X, K*W*4 < 2^31 (ldx=%lld)", (long long)(K * W), (long long)ldx);
+    if (algo == GM_ALGO_AUTO) algo = GM_ALGO_STREAM;
+    if (algo != GM_ALGO_STREAM)
+      return fail(GM_ERR_UNSUPPORTED, "panel layout: streaming algorithm only (algo %d)", algo);
+  }
+  const int V = panels ? 4 : pick_vec(X, d, ldx);
   // AUTO: Gram-space (split bf16) for gm2 at K <= 256 on large d, kept if its
   // accuracy guard passes (run_gram); streaming otherwise.  X is read twice
   // instead of n+1 times (profiles/r01_cmp_algos.txt, r02_gram_split.txt).
@@ -504,7 +526,9 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   }
   if (algo == GM_ALGO_RESIDENT)
     return fail(GM_ERR_UNSUPPORTED, "resident kernel: problem too large, sharded or host noise");
-  if (algo == GM_ALGO_AUTO || algo == GM_ALGO_STREAM) {
+  if (panels) {
+    // cfg fixed above
+  } else if (algo == GM_ALGO_AUTO || algo == GM_ALGO_STREAM) {
     if (pick_cfg(K, V, ldx, &cfg)) algo = GM_ALGO_STREAM;
     else if (algo == GM_ALGO_STREAM)
       return fail(GM_ERR_UNSUPPORTED, "streaming pass supports K <= 2048 (K=%lld)", (long long)K);
@@ -527,7 +551,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   const int init_mode = o->mode == GM_MODE_AIRCOMP ? 2 : 1;   // ||x_k||^2 only for AirComp
 
   int nb_step, nb_init;
-  const PassCfg cfg_i = light_cfg(K, cfg);
+  const PassCfg cfg_i = panels ? cfg : light_cfg(K, cfg);
   if (algo == GM_ALGO_STREAM) {
     const int J = cfg.LPR * cfg.V, Ji = cfg_i.LPR * cfg_i.V;
     const int64_t nch = (d + J - 1) / J, nchi = (d + Ji - 1) / Ji;
@@ -607,6 +631,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       a.g_old = g_old; a.g_new = g_new; a.coef = w.coef; a.st = w.st;
       a.slab = w.slab; a.slab_stride = S;
       a.noise = noise_kind; a.hnoise = w.hnoise; a.seed = o->seed; a.iter = t; a.col_off = col_off;
+      a.panel_stride = panels ? ldx : 0;
       HIPCHK(launch_pass(init ? cfg_i : cfg, init ? init_mode : 0, init ? nb_init : nb_step, a, s));
       if (!init) { rc2 = record_pass_end(c, s, e0, e1); if (rc2) return rc2; }
       HIPCHK(launch_slab_reduce(w.slab, init ? nb_init : nb_step, S, w.sums, w.st, s));

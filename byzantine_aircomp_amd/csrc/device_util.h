@@ -25,12 +25,14 @@ __device__ __forceinline__ void load_cols(const float* __restrict__ p, float (&o
 }
 
 // V consecutive floats at byte offset `off` from the wave-uniform `base`, through
-// a raw buffer resource (num_records 2^31: offsets >= 0x80000000 read 0),
+// a raw buffer resource (offsets >= nrec read 0),
 // streamed (slc).  One VGPR of address per load instead of a 64-bit pointer.
+// `nrec` = the resource's size in bytes (offsets >= nrec read 0).
 template <int V>
-__device__ __forceinline__ void load_rows(const float* base, uint32_t off, float (&o)[V]) {
+__device__ __forceinline__ void load_rows(const float* base, uint32_t off, float (&o)[V],
+                                          int nrec = 0x7fffffff) {
   const __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x80000000, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, nrec, 0x00020000);
   if constexpr (V == 4) {
     typedef float f4 __attribute__((ext_vector_type(4)));
     const f4 v = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2));

@@ -50,6 +50,9 @@ struct PassArgs {
   // g_old, g_new advance by these element strides, coef by K, st by 1, slab by
   // gridDim.x * slab_stride, the Philox seed by p * kSeedStride.  0 / unused for P = 1.
   int64_t x_ps, gold_ps, gnew_ps;
+  // > 0: X is in the panel layout [ceil(d/J)][K][J] with this many elements
+  // between panels (J = the tile's chunk width); 0: row-major [K][ldx].
+  int64_t panel_stride;
 };
 
 constexpr uint64_t kSeedStride = 0x9E3779B97F4A7C15ull;

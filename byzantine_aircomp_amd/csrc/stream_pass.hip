@@ -34,12 +34,18 @@ struct Tile {
   float hn;      // STEP finisher thread, host noise: its column's draw
 };
 
-// MODE: 0 step, 1 init, 2 init + ||x_k||^2.  PIPE: chunk c+1's loads are in
-// flight while chunk c is reduced (two tiles of registers).
+// MODE: 0 step, 1 init, 2 init + ||x_k||^2, 3 Gram closing sum.  SCHED 0: load a
+// chunk, then reduce it; 1 (PIPE): chunk c+1's loads are in flight while chunk
+// c is reduced (two tiles of registers); 2 (ROLL): row i of chunk c+1 is loaded
+// into the registers phase B has just freed (one tile).
 // OCC: blocks per CU the register budget is capped for (2 -> <= 64 VGPRs at
 // 16 waves); with OCC > 1 the row weights are read from LDS instead of VGPRs.
-template <int V, int NW, int LPR, int R, int MODE, bool PIPE, int OCC = 1>
+// PANEL: X is the panel layout [nch][K][J] (a.panel_stride elements between
+// panels, rows J apart): a chunk is one contiguous block, every row offset in
+// it fits the 32-bit lane offset, and the HBM stream is sequential.
+template <int V, int NW, int LPR, int R, int MODE, int SCHED, int OCC = 1, bool PANEL = false>
 __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs a) {
+  constexpr bool PIPE = SCHED == 1, ROLL = SCHED == 2;
   constexpr bool SUM_ONLY = MODE == 3;     // closing pass of the Gram variant: g = sum c_k x_k
   constexpr bool INIT = MODE == 1 || MODE == 2;
   constexpr bool WANT_R = MODE == 2;
@@ -75,27 +81,18 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
   const int64_t nch = (d + J - 1) / J;
   const int64_t grid = gridDim.x;
 
-  // Row r of this thread = wave-uniform row-group base (a buffer resource in
-  // SGPRs, rebuilt per chunk by scalar adds) + ONE 32-bit lane byte offset shared
-  // by all R rows.  Rows >= K and columns >= d get an out-of-range offset: the
-  // buffer unit returns 0 for them, so every load is unconditional and no
-  // per-row 64-bit address is kept in VGPRs.
-  // Rows: SGPR base + lane offset through global_load (measured 1.8 % faster than
-  // buffer_load with one shared VGPR offset, -DGMK_BUFFER_LOADS, on the C3 pass:
-  // 6.90 vs 7.03 ms, same box; profiles/r02_ab_loads.txt).
+  // Row r of this thread = wave-uniform row-group base (SGPRs) + ONE 32-bit lane
+  // offset shared by all R rows (measured 1.8 % faster than buffer_load with one
+  // shared VGPR offset on the C3 pass: 6.90 vs 7.03 ms, same box;
+  // profiles/r02_ab_loads.txt).
   bool rval[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) rval[i] = rg + (int64_t)NRG * i < K;
-#ifndef GMK_BUFFER_LOADS
   const float* base[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) base[i] = a.X + (int64_t)(w * QW + NRG * i) * a.ldx;
   const uint32_t goff = (uint32_t)q * (uint32_t)a.ldx;
-#else
-  const uint32_t loff = ((uint32_t)q * (uint32_t)a.ldx + (uint32_t)(c * V)) * 4u;
-  const int64_t row_step = (int64_t)NRG * a.ldx;   // elements between row groups i, i+1
-  const float* wbase = a.X + (int64_t)(w * QW) * a.ldx;
-#endif
+  const uint32_t poff = ((uint32_t)q * J + (uint32_t)(c * V)) * 4u;   // PANEL: bytes from the wave's rows
 
   float wt[OCC > 1 ? 1 : R];
   float a_noise = 0.f;
@@ -110,29 +107,33 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
     a_noise = a.st->a_noise;
   }
 
-  auto fetch = [&](int64_t ch, T& t) {
+  auto fetch_row = [&](int64_t ch, T& t, int i) {
+    if constexpr (PANEL) {
+      // One buffer resource per (chunk, row group i) in SGPRs, sized to the rows
+      // that exist (rows >= K read 0 through the range check), + the one lane
+      // offset (columns >= d: an out-of-range offset).  Branch-free.
+      constexpr int64_t GB = (int64_t)NRG * J * 4;   // bytes per row group
+      const int64_t wb = (int64_t)(w * QW) * J * 4 + i * GB;   // this wave's rows, bytes
+      const int64_t nrec = (int64_t)K * J * 4 - wb;
+      const uint32_t vo = (ch < nch && ch * J + c * V < d) ? poff : 0x80000000u;
+      load_rows<V>(reinterpret_cast<const float*>(
+                       reinterpret_cast<const char*>(a.X + ch * a.panel_stride) + wb),
+                   vo, t.x[i], nrec <= 0 ? 0 : nrec > 0x7fffffff ? 0x7fffffff : (int)nrec);
+      return;
+    }
     const int64_t col = ch * J + (int64_t)c * V;
     const bool cval = ch < nch && col < d;   // V | d: a lane's group is all-in or all-out
-#ifndef GMK_BUFFER_LOADS
-    const uint32_t off = goff + (uint32_t)col;
+    if (cval && rval[i]) {
+      load_cols<V>(base[i] + (goff + (uint32_t)col), t.x[i]);
+    } else {
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-      if (cval && rval[i]) {
-        load_cols<V>(base[i] + off, t.x[i]);
-      } else {
-#pragma unroll
-        for (int v = 0; v < V; ++v) t.x[i][v] = 0.f;
-      }
+      for (int v = 0; v < V; ++v) t.x[i][v] = 0.f;
     }
-#else
-    const float* cb = wbase + (ch < nch ? ch * J : 0);
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const uint32_t off = (cval && rval[i]) ? loff : 0x80000000u;   // OOB reads 0
-      load_rows<V>(cb + i * row_step, off, t.x[i]);
-    }
-#endif
+  };
+  auto fetch_aux = [&](int64_t ch, T& t) {
     if constexpr (INIT) {
+      const int64_t col = ch * J + (int64_t)c * V;
+      const bool cval = ch < nch && col < d;
 #pragma unroll
       for (int v = 0; v < V; ++v) t.g[v] = cval ? a.g_old[col + v] : 0.f;
     } else {
@@ -142,13 +143,21 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
       t.hn = (fin && a.noise == 2) ? a.hnoise[gj] : 0.f;
     }
   };
+  auto fetch = [&](int64_t ch, T& t) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) fetch_row(ch, t, i);
+    fetch_aux(ch, t);
+  };
 
   double row_acc[RPL], row_acc2[RPL];
 #pragma unroll
   for (int m = 0; m < RPL; ++m) row_acc[m] = row_acc2[m] = 0.0;
   double mv_acc = 0.0, gn_acc = 0.0;
 
-  auto process = [&](int64_t ch, T& t) {
+  // ROLL: row i of chunk `nxt` is loaded into t.x[i] as soon as phase B has
+  // consumed row i of chunk ch, so the next chunk's loads are in flight during
+  // phase B, the row reductions and the next chunk's barriers (no second tile).
+  auto process = [&](int64_t ch, T& t, int64_t nxt) {
     float gv[V];
     if constexpr (INIT) {
 #pragma unroll
@@ -205,33 +214,34 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
 #pragma unroll
       for (int v = 0; v < V; ++v) gv[v] = s_g[c * V + v];
     }
-    if constexpr (SUM_ONLY) return;
-    // phase B: squared distances of this thread's rows to the (new) iterate.
-    float e[R];
+    if constexpr (SUM_ONLY) {
+      if constexpr (ROLL) fetch(nxt, t);
+      return;
+    }
+    // phase B: squared distances of this thread's rows to the (new) iterate
+    // (+ ||x_k||^2 for the AirComp INIT pass).
+    float e[R], e2[WANT_R ? R : 1];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      float s = 0.f;
+      float s = 0.f, s2 = 0.f;
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const float tt = t.x[i][v] - gv[v];
         s = fmaf(tt, tt, s);
+        if constexpr (WANT_R) s2 = fmaf(t.x[i][v], t.x[i][v], s2);
       }
       e[i] = s;
+      if constexpr (WANT_R) e2[i] = s2;
+      if constexpr (ROLL) fetch_row(nxt, t, i);
     }
+    if constexpr (ROLL) fetch_aux(nxt, t);
     transpose_reduce<LPR, R>(e, c);
 #pragma unroll
     for (int m = 0; m < RPL; ++m) row_acc[m] += (double)e[m];
     if constexpr (WANT_R) {
+      transpose_reduce<LPR, R>(e2, c);
 #pragma unroll
-      for (int i = 0; i < R; ++i) {
-        float s = 0.f;
-#pragma unroll
-        for (int v = 0; v < V; ++v) s = fmaf(t.x[i][v], t.x[i][v], s);
-        e[i] = s;
-      }
-      transpose_reduce<LPR, R>(e, c);
-#pragma unroll
-      for (int m = 0; m < RPL; ++m) row_acc2[m] += (double)e[m];
+      for (int m = 0; m < RPL; ++m) row_acc2[m] += (double)e2[m];
     }
   };
 
@@ -241,16 +251,20 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
     fetch(ch, ta);
     for (; ch < nch; ch += 2 * grid) {
       fetch(ch + grid, tb);
-      process(ch, ta);
+      process(ch, ta, -1);
       if (ch + grid >= nch) break;       // block-uniform
       fetch(ch + 2 * grid, ta);
-      process(ch + grid, tb);
+      process(ch + grid, tb, -1);
     }
+  } else if constexpr (ROLL) {
+    T t;
+    fetch(blockIdx.x, t);
+    for (int64_t ch = blockIdx.x; ch < nch; ch += grid) process(ch, t, ch + grid);
   } else {
     for (int64_t ch = blockIdx.x; ch < nch; ch += grid) {
       T t;
       fetch(ch, t);
-      process(ch, t);
+      process(ch, t, -1);
     }
   }
 
@@ -289,9 +303,9 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
 }
 
 // ---------------------------------------------------------------------------
-// Launch plumbing.  GMAGG_PASS_VARIANT: -1 auto (default), 0 plain, 1 pipelined.
+// Launch plumbing.  GMAGG_PASS_VARIANT: -1 auto (default), 0 plain, 1 pipelined
+// (-DGMK_PIPE_VARIANT builds only), 2 rolling prefetch.
 
-#ifdef GMK_PIPE_VARIANT
 static int pass_variant() {
   static const int v = [] {
     const char* e = getenv("GMAGG_PASS_VARIANT");
@@ -299,27 +313,37 @@ static int pass_variant() {
   }();
   return v;
 }
-#endif
 
 template <int V, int NW, int LPR, int R, int MODE, int OCC>
-static const void* pass_fn() {
+static const void* pass_fn(bool panel) {
   // Measured on MI355X (profiles/r01_ab_pass.txt, r01_pipe_sweep.txt): the plain
-  // pass is as fast or faster at every K, so the two-tile variant is only built
-  // with -DGMK_PIPE_VARIANT for A/B runs.
+  // pass is as fast or faster than the two-tile PIPE variant at every K, so that
+  // one is only built with -DGMK_PIPE_VARIANT for A/B runs.
+  if constexpr (V == 4) {
+    if (panel) {
+      if (pass_variant() == 2)
+        return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 2, OCC, true>);
+      return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 0, OCC, true>);
+    }
+  } else if (panel) {
+    return nullptr;
+  }
 #ifdef GMK_PIPE_VARIANT
   if (pass_variant() == 1)
-    return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, true, OCC>);
+    return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 1, OCC>);
 #endif
-  return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, false, OCC>);
+  if (pass_variant() == 2)
+    return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 2, OCC>);
+  return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 0, OCC>);
 }
 
 template <int V, int NW, int LPR, int R, int OCC>
-static const void* pass_fn_mode(int mode) {
+static const void* pass_fn_mode(int mode, bool panel) {
   switch (mode) {
-    case 0: return pass_fn<V, NW, LPR, R, 0, OCC>();
-    case 1: return pass_fn<V, NW, LPR, R, 1, OCC>();
-    case 2: return pass_fn<V, NW, LPR, R, 2, OCC>();
-    default: return pass_fn<V, NW, LPR, R, 3, OCC>();
+    case 0: return pass_fn<V, NW, LPR, R, 0, OCC>(panel);
+    case 1: return pass_fn<V, NW, LPR, R, 1, OCC>(panel);
+    case 2: return pass_fn<V, NW, LPR, R, 2, OCC>(panel);
+    default: return pass_fn<V, NW, LPR, R, 3, OCC>(panel);
   }
 }
 
@@ -332,10 +356,10 @@ static const void* pass_fn_mode(int mode) {
   X_(V_, 8, 32, 4, 1) X_(V_, 16, 8, 8, 2) X_(V_, 16, 16, 16, 1) X_(V_, 8, 8, 16, 2)          \
   X_(V_, 16, 32, 8, 2) X_(V_, 16, 64, 4, 2) X_(V_, 16, 64, 16, 1) X_(V_, 8, 16, 8, 2)
 
-static const void* pass_kernel(const PassCfg& cfg, int mode) {
+static const void* pass_kernel(const PassCfg& cfg, int mode, bool panel = false) {
 #define GMK_CASE(V_, W_, L_, R_, O_)                                                 \
   if (cfg.V == V_ && cfg.NW == W_ && cfg.LPR == L_ && cfg.R == R_ && cfg.OCC == O_) \
-    return pass_fn_mode<V_, W_, L_, R_, O_>(mode);
+    return pass_fn_mode<V_, W_, L_, R_, O_>(mode, panel);
   GMK_FOR_EACH_CFG(GMK_CASE, 4)
   GMK_FOR_EACH_CFG(GMK_CASE, 2)
   GMK_FOR_EACH_CFG(GMK_CASE, 1)
@@ -347,7 +371,7 @@ bool pass_cfg_supported(const PassCfg& cfg) { return pass_kernel(cfg, 0) != null
 
 hipError_t launch_pass(const PassCfg& cfg, int mode, int grid, const PassArgs& a, hipStream_t s,
                        int problems) {
-  const void* fn = pass_kernel(cfg, mode);
+  const void* fn = pass_kernel(cfg, mode, a.panel_stride > 0);
   if (!fn) return hipErrorInvalidValue;
   void* args[] = {const_cast<PassArgs*>(&a)};
   return hipLaunchKernel(fn, dim3(grid, problems), dim3(cfg.NW * 64), args, 0, s);

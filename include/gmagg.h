@@ -20,7 +20,12 @@
  *   - A context is used by one host thread at a time.
  *
  * Layout: X is row-major [K][ldx] fp32, row k = client k's flattened update
- * (model.parameters() order, MNIST_Air_weight.py:206-209), ldx >= d.
+ * (model.parameters() order, MNIST_Air_weight.py:206-209), ldx >= d — the
+ * reference's own torch.stack layout.  gm_weiszfeld_f32 also takes the panel
+ * layout (gm_opts.layout = GM_LAYOUT_PANELS): X as [ceil(d/W)][K][W] with
+ * W = gm_panel_width(K) and ldx = elements between panels (>= K*W); element
+ * (k, j) at X[(j/W)*ldx + k*W + j%W].  Each streaming-pass chunk is then one
+ * contiguous block of HBM.
  */
 #ifndef GMAGG_H
 #define GMAGG_H
@@ -50,6 +55,12 @@ enum gm_mode {
 enum gm_noise_source {
     GM_NOISE_PHILOX = 0,      /* on-device Philox4x32-10, keyed (seed, iteration, global index) */
     GM_NOISE_HOST = 1         /* caller supplies the reference's draws through noise_cb */
+};
+
+enum gm_layout {
+    GM_LAYOUT_ROWS = 0,       /* [K][ldx] row-major (the reference's torch.stack of rows) */
+    GM_LAYOUT_PANELS = 1      /* [ceil(d/W)][K][W], W = gm_panel_width(K), ldx = panel stride;
+                                 streaming algorithm only (AUTO -> STREAM) */
 };
 
 enum gm_algo {
@@ -88,7 +99,7 @@ typedef struct gm_opts {
     gm_noise_cb noise_cb;     /* GM_NOISE_HOST */
     void* noise_user;
     int32_t check_every;      /* host convergence poll interval in iterations; 0 = auto */
-    int32_t reserved;
+    int32_t layout;           /* gm_layout of X (gm_weiszfeld_f32 only; batched: ROWS) */
 } gm_opts;
 
 typedef struct gm_result {
@@ -122,6 +133,10 @@ int gm_ctx_init_rccl(gm_ctx* ctx, const void* unique_id_128, int nranks, int ran
 int gm_weiszfeld_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t ldx,
                      const float* guess0, float* out, const gm_opts* opts,
                      gm_result* result, void* stream);
+
+/* Panel width W of the GM_LAYOUT_PANELS layout for K clients (the streaming
+ * tile's chunk width: 32 columns at 512 < K <= 1024); 0 if K is unsupported. */
+int64_t gm_panel_width(int64_t K);
 
 /* Batched independent problems (BASELINE config C5, the draw.ipynb-style sweep
  * over many small aggregations): problem p aggregates the K rows at X + p*ldp

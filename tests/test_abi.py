@@ -82,3 +82,15 @@ def test_errors_are_reported_not_raised():
     assert b"NULL" in lib.gm_last_error()
     rc = lib.gm_ctx_set_shard(None, 10, 0)
     assert rc == -1
+
+
+def test_panel_width_table():
+    """gm_panel_width is the streaming tile's chunk width (no GPU needed)."""
+    lib = _lib.load()
+    assert lib.gm_panel_width(0) == 0
+    assert lib.gm_panel_width(1000) == 32
+    assert lib.gm_panel_width(50) in (64, 128, 256)
+    assert lib.gm_panel_width(4096) == 0
+    for K in (1, 16, 17, 100, 256, 257, 600, 1024, 2048):
+        W = lib.gm_panel_width(K)
+        assert W > 0 and 256 % W == 0          # shard boundaries (256-aligned) stay on panels

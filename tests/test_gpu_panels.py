@@ -1,0 +1,89 @@
+"""The panel layout (ClientPanels, GM_LAYOUT_PANELS) on the GPU.
+
+Same values, same chunks, same reduction order as the row-major call, so the
+aggregate, the iteration count and the last movement must be BIT-identical to
+gm2 / gm on the [K, d] tensor — which the row-major tests pin to the reference
+(test_gpu_weiszfeld.py) — plus the reference's golden vectors directly.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_case, golden_names, rel_l2
+
+pytestmark = pytest.mark.gpu
+
+
+def bz():
+    import byzantine_aircomp_amd as m
+    return m
+
+
+def _data(K, d, seed, byz=0.2):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(K, d, generator=g) * 0.05
+    nb = int(K * byz)
+    if nb:
+        X[K - nb:] = torch.randn(nb, d, generator=g) * 0.5 + 0.25
+    g0 = torch.randn(d, generator=g) * 0.01
+    return X.cuda(), g0.cuda()
+
+
+@pytest.mark.parametrize("K,d", [(1, 5), (7, 1), (50, 7850), (50, 4099), (129, 1000),
+                                 (300, 2051), (1000, 4096), (1000, 70001), (1500, 3000)])
+@pytest.mark.parametrize("agg", ["gm2", "gm"])
+def test_panels_bit_identical_to_rows(K, d, agg):
+    X, g0 = _data(K, d, seed=K * 7 + d)
+    P = bz().ClientPanels.from_rows(X)
+    assert torch.equal(P.to_rows(), X)
+    opts = {"maxiter": 50, "tol": 1e-5, "guess": g0, "algo": "stream"}
+    if agg == "gm":
+        opts.update(noise_var=1e-2, seed=99)
+    f = getattr(bz(), agg)
+    a = f(X, dict(opts))
+    ra = bz().aggregators.last_result
+    b = f(P, dict(opts))
+    rb = bz().aggregators.last_result
+    assert rb.algo == "stream"
+    assert torch.equal(a, b)
+    assert (ra.iters, ra.converged) == (rb.iters, rb.converged)
+    assert ra.last_movement == rb.last_movement or (np.isnan(ra.last_movement)
+                                                    and np.isnan(rb.last_movement))
+
+
+@pytest.mark.parametrize("name", golden_names("gm2"))
+def test_panels_match_reference_gm2(name):
+    meta, arr = golden_case(name)
+    o = dict(meta["options"])
+    if o.get("maxiter", 200) == 0:
+        pytest.skip("maxiter 0 returns the guess object (covered by the row-major test)")
+    if meta.get("guess_supplied"):
+        o["guess"] = torch.from_numpy(arr["guess"].copy()).cuda()
+    P = bz().ClientPanels.from_rows(torch.from_numpy(arr["X"].copy()).cuda())
+    out = bz().gm2(P, o)
+    res = bz().aggregators.last_result
+    assert rel_l2(out.cpu().numpy(), arr["out"]) <= 1e-5
+    assert abs(res.iters - meta["iters"]) <= 1
+
+
+def test_panels_store_rows_and_default_guess():
+    K, d = 40, 1234
+    X, _ = _data(K, d, seed=5)
+    P = bz().ClientPanels(K, d)
+    for k in range(K):
+        P.store(k, X[k])
+    assert torch.equal(P.to_rows(), X)
+    assert torch.equal(P.row(3), X[3])
+    a = bz().gm2(X, {"maxiter": 20, "guess": X.mean(dim=0)})
+    b = bz().gm2(P, {"maxiter": 20, "guess": X.mean(dim=0)})
+    assert torch.equal(a, b)
+    c = bz().gm2(P, {"maxiter": 20})          # guess = column mean of the panels
+    assert rel_l2(c.cpu().numpy(), a.cpu().numpy()) <= 1e-6
+
+
+def test_panels_reject_non_streaming_algos():
+    X, g0 = _data(64, 512, seed=1)
+    P = bz().ClientPanels.from_rows(X)
+    for algo in ("gram", "twopass", "resident"):
+        with pytest.raises(RuntimeError):
+            bz().gm2(P, {"maxiter": 5, "guess": g0, "algo": algo})
