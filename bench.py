@@ -57,9 +57,13 @@ def parse():
     p.add_argument("--agg", default="gm2", choices=["gm2", "gm"])
     p.add_argument("--var", type=float, default=None, help="gm noise variance (None = no AWGN)")
     p.add_argument("--maxiter", type=int, default=1000)
-    p.add_argument("--layout", default="rows", choices=["rows", "panels"],
+    p.add_argument("--layout", default="auto", choices=["auto", "rows", "panels"],
                    help="client matrix layout: rows = the reference's [K, d] stack; panels = "
-                        "ClientPanels [ceil(d/W)][K][W] (streaming algorithm)")
+                        "ClientPanels [ceil(d/W)][K][W] (streaming algorithm); auto = panels "
+                        "for the streaming workloads (c3), rows otherwise.  The other layout "
+                        "is timed too (alt_layout in the JSON line).")
+    p.add_argument("--alt-steps", type=int, default=None,
+                   help="steps for the other layout's measurement (0 = skip)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-d", type=int, default=2_000_000, help="CPU sample width")
     p.add_argument("--dist", action="store_true",
@@ -75,22 +79,23 @@ def shard_range(d, n, r, align=256):
     return lo, min(d, lo + per)
 
 
-def pmc_traffic(workload):
+def pmc_traffic(workload, layout):
     """Per-launch HBM bytes of the STEP pass from the newest committed PMC summary
-    (rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same bench workload;
-    tools/pmc_summary.py applies the gfx950 FETCH_SIZE x2 correction)."""
+    (rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same bench workload and
+    layout; tools/pmc_summary.py applies the gfx950 FETCH_SIZE x2 correction)."""
     import glob
     import re
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}.json")))
-    if not files:
-        return None, None
-    data = json.load(open(files[-1]))
-    for name, row in data["kernels"].items():
-        m = re.search(r"weiszfeld_pass<([^>]*)>", name)
-        targs = m.group(1).split(", ") if m else []
-        mode = targs[4] if len(targs) == 7 else (targs[-2] if targs else None)   # <V,NW,LPR,R,MODE,PIPE,OCC>
-        if mode == "0":
-            return row["hbm_bytes_per_launch"] / 1e9, os.path.relpath(files[-1], ROOT)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}*.json")))
+    for path in reversed(files):
+        data = json.load(open(path))
+        for name, row in data["kernels"].items():
+            m = re.search(r"weiszfeld_pass<([^>]*)>", name)
+            if not m:
+                continue
+            targs = m.group(1).split(", ")        # <V,NW,LPR,R,MODE,SCHED,OCC[,PANEL]>
+            panel = len(targs) == 8 and targs[7] == "true"
+            if targs[4] == "0" and panel == (layout == "panels"):
+                return row["hbm_bytes_per_launch"] / 1e9, os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -161,40 +166,67 @@ def main():
     if args.agg == "gm":
         opts.update(noise_var=args.var, seed=2021)
     agg = bz.gm2 if args.agg == "gm2" else bz.gm
-    Xin = X
-    if args.layout == "panels":
-        Xin = bz.ClientPanels.from_rows(X)      # same values, panel layout (packed once)
+    layout = args.layout
+    if layout == "auto":
+        layout = "panels" if args.workload.startswith("c3") and args.algo in ("auto", "stream") \
+            else "rows"
+    panels = None
 
-    def step():
-        return agg(Xin, opts)
+    def inputs(lay):
+        nonlocal panels
+        if lay == "rows":
+            return X
+        if panels is None:
+            panels = bz.ClientPanels.from_rows(X)     # same values, panel layout (packed once)
+        return panels
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist_path:
-        torch.distributed.barrier()
-    torch.cuda.synchronize(dev)
-    ctx.pass_timing(True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    torch.cuda.synchronize(dev)
-    if dist_path:
-        torch.distributed.barrier()
-    t1 = time.perf_counter()
-    pass_ms, launches = ctx.pass_timing(False)
-    res = bz.aggregators.last_result
-    elapsed = t1 - t0
-    if dist_path:
-        t = torch.tensor([elapsed], device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def measure(Xin, steps, warmup):
+        """warmup untimed aggregations, then `steps` timed between barriers +
+        device syncs; returns (max-over-ranks seconds, pass ms, launches, result)."""
+        for _ in range(warmup):
+            agg(Xin, opts)
+        torch.cuda.synchronize(dev)
+        if dist_path:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+        ctx.pass_timing(True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = agg(Xin, opts)
+        torch.cuda.synchronize(dev)
+        if dist_path:
+            torch.distributed.barrier()
+        t1 = time.perf_counter()
+        pass_ms, launches = ctx.pass_timing(False)
+        res = bz.aggregators.last_result
+        elapsed = t1 - t0
+        if dist_path:
+            t = torch.tensor([elapsed], device=dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            elapsed = float(t.item())
+        del out
+        return elapsed, pass_ms, launches, res
+
+    elapsed, pass_ms, launches, res = measure(inputs(layout), args.steps, args.warmup)
+    alt = None
+    alt_layout = "rows" if layout == "panels" else "panels"
+    alt_steps = args.alt_steps if args.alt_steps is not None else max(3, args.steps // 4)
+    if alt_steps > 0 and (alt_layout == "rows" or (args.algo in ("auto", "stream")
+                                                   and bz.panel_width(K) > 0)):
+        a_el, a_ms, a_n, a_res = measure(inputs(alt_layout), alt_steps, 1)
+        a_pass = (a_ms / 1e3) / max(a_n, 1)
+        alt = {"layout": alt_layout, "value": alt_steps / a_el, "steps": alt_steps,
+               "ms_per_step": 1e3 * a_el / alt_steps, "iters": a_res.iters, "algo": a_res.algo,
+               "avg_launch_us": a_pass * 1e6,
+               "frac": 4.0 * K * d / a_pass / 1e9 / HBM_PEAK_GBS}
+    if panels is not None and layout == "rows":
+        panels = None
 
     if rank == 0:
         per_launch_bytes = 4.0 * K * d
         avg_pass_s = (pass_ms / 1e3) / max(launches, 1)
         achieved = per_launch_bytes / avg_pass_s / 1e9
-        traffic, traffic_src = pmc_traffic(args.workload) if world == 1 else (None, None)
+        traffic, traffic_src = pmc_traffic(args.workload, layout) if world == 1 else (None, None)
         if res.algo in ("gram", "gram_f32"):
             # dominant kernel = the Gram partial: upper-triangle 32x32 tiles of the
             # K-padded Gram, 2 FLOP per MAC, d_local columns; the split kernel issues
@@ -222,7 +254,7 @@ def main():
             roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                     "traffic_unit": "GB per launch", "traffic_source": traffic_src,
-                    "kernel": "weiszfeld_pass (STEP)", "launches_timed": launches,
+                    "kernel": f"weiszfeld_pass (STEP, {layout})", "launches_timed": launches,
                     "avg_launch_us": avg_pass_s * 1e6,
                     "algorithmic_bytes_per_launch": per_launch_bytes}
         line = {
@@ -243,16 +275,16 @@ def main():
                                    f"Byzantine, tol 1e-5, maxiter {args.maxiter}"
                                    + (f", noise_var {args.var}" if args.agg == "gm" else ""),
                        "K": K, "d": d_total, "byzantine": B, "iters": res.iters,
-                       "algo": res.algo, "layout": args.layout, "parallelism": f"d-shard x{world}" if dist_path else "none",
+                       "algo": res.algo, "layout": layout, "parallelism": f"d-shard x{world}" if dist_path else "none",
                        "passes_per_aggregation": 2 if res.algo.startswith("gram") else res.iters + 1},
             "roofline": roof,
             "cpu_baseline": None,
+            "alt_layout": alt,
         }
         if world == 1 and not args.no_cpu and args.agg == "gm2":
             dc = min(args.cpu_d, d)
             line["cpu_baseline"] = cpu_baseline(X[:, :dc].contiguous(), g0[:dc], res.iters, d_total)
         print(json.dumps(line), file=json_out, flush=True)
-    del out
     torch.cuda.synchronize(dev)
     ctx.close()                       # RCCL communicator + workspace, before the process group
     if dist_path:

@@ -466,7 +466,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
                      const float* guess0, float* out, const gm_opts* o, gm_result* res,
                      void* stream) {
   if (!c || !o || !out || !guess0) return fail(GM_ERR_INVALID, "gm_weiszfeld_f32: NULL argument");
-  if (K < 1 || d < 1 || ldx < d || (!X)) return fail(GM_ERR_INVALID, "gm_weiszfeld_f32: bad shape K=%lld d=%lld ldx=%lld", (long long)K, (long long)d, (long long)ldx);
+  if (K < 1 || d < 1 || (ldx < d && o && o->layout == GM_LAYOUT_ROWS) || (!X)) return fail(GM_ERR_INVALID, "gm_weiszfeld_f32: bad shape K=%lld d=%lld ldx=%lld", (long long)K, (long long)d, (long long)ldx);
   if (o->maxiter < 0) return fail(GM_ERR_INVALID, "gm_weiszfeld_f32: maxiter < 0");
   if (o->mode != GM_MODE_IDEAL && o->mode != GM_MODE_AIRCOMP)
     return fail(GM_ERR_INVALID, "gm_weiszfeld_f32: unknown mode %d", o->mode);

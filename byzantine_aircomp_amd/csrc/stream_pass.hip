@@ -119,6 +119,11 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
       load_rows<V>(reinterpret_cast<const float*>(
                        reinterpret_cast<const char*>(a.X + ch * a.panel_stride) + wb),
                    vo, t.x[i], nrec <= 0 ? 0 : nrec > 0x7fffffff ? 0x7fffffff : (int)nrec);
+      if ((ch + 1) * J > d) {   // last chunk (block-uniform): padding columns read as 0
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+          if (ch * J + c * V + v >= d) t.x[i][v] = 0.f;
+      }
       return;
     }
     const int64_t col = ch * J + (int64_t)c * V;
@@ -134,8 +139,13 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
     if constexpr (INIT) {
       const int64_t col = ch * J + (int64_t)c * V;
       const bool cval = ch < nch && col < d;
+      if (!PANEL || (ch + 1) * J <= d) {   // row-major: V | d, a lane's group is all-in or all-out
 #pragma unroll
-      for (int v = 0; v < V; ++v) t.g[v] = cval ? a.g_old[col + v] : 0.f;
+        for (int v = 0; v < V; ++v) t.g[v] = cval ? a.g_old[col + v] : 0.f;
+      } else {                             // panels: d need not be a multiple of V
+#pragma unroll
+        for (int v = 0; v < V; ++v) t.g[v] = (ch < nch && col + v < d) ? a.g_old[col + v] : 0.f;
+      }
     } else {
       const int64_t gj = ch * J + tid;
       const bool fin = tid < J && ch < nch && gj < d;
@@ -319,9 +329,13 @@ static const void* pass_fn(bool panel) {
   // Measured on MI355X (profiles/r01_ab_pass.txt, r01_pipe_sweep.txt): the plain
   // pass is as fast or faster than the two-tile PIPE variant at every K, so that
   // one is only built with -DGMK_PIPE_VARIANT for A/B runs.
+  // Panels: the rolling-prefetch STEP pass (6.44-6.56 vs 6.63 ms at C3); its INIT
+  // variants spill (29 VGPRs at the C3 tile) and run slower, so INIT stays plain
+  // (profiles/r03_panels_ab.txt).
   if constexpr (V == 4) {
     if (panel) {
-      if (pass_variant() == 2)
+      const int pv = pass_variant();
+      if (pv == 2 || (pv < 0 && MODE == 0))
         return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 2, OCC, true>);
       return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 0, OCC, true>);
     }

@@ -1,9 +1,10 @@
 """The panel layout (ClientPanels, GM_LAYOUT_PANELS) on the GPU.
 
-Same values, same chunks, same reduction order as the row-major call, so the
-aggregate, the iteration count and the last movement must be BIT-identical to
-gm2 / gm on the [K, d] tensor — which the row-major tests pin to the reference
-(test_gpu_weiszfeld.py) — plus the reference's golden vectors directly.
+Same values, same chunks, same reduction order as the row-major call with the
+float4 tile (d % 4 == 0), so the aggregate, the iteration count and the last
+movement must be BIT-identical to gm2 / gm on the [K, d] tensor — which the
+row-major tests pin to the reference (test_gpu_weiszfeld.py); other d within
+rounding; plus the reference's golden vectors directly.
 """
 import numpy as np
 import pytest
@@ -45,10 +46,18 @@ def test_panels_bit_identical_to_rows(K, d, agg):
     b = f(P, dict(opts))
     rb = bz().aggregators.last_result
     assert rb.algo == "stream"
-    assert torch.equal(a, b)
-    assert (ra.iters, ra.converged) == (rb.iters, rb.converged)
-    assert ra.last_movement == rb.last_movement or (np.isnan(ra.last_movement)
-                                                    and np.isnan(rb.last_movement))
+    if d % 4 == 0 and not 128 < K <= 256:
+        # the row-major call runs the same float4 tile: same chunks, same order
+        # (at 128 < K <= 256 its INIT pass takes a wider tile, api.hip light_cfg)
+        assert torch.equal(a, b)
+        assert (ra.iters, ra.converged) == (rb.iters, rb.converged)
+        assert ra.last_movement == rb.last_movement or (np.isnan(ra.last_movement)
+                                                        and np.isnan(rb.last_movement))
+    else:
+        # row-major runs another tile here (float2/float1 for d % 4 != 0, or the
+        # wider INIT tile): other summation grouping, equal to rounding
+        assert rel_l2(b.cpu().numpy(), a.cpu().numpy()) <= 1e-6
+        assert abs(ra.iters - rb.iters) <= 1
 
 
 @pytest.mark.parametrize("name", golden_names("gm2"))
@@ -67,14 +76,15 @@ def test_panels_match_reference_gm2(name):
 
 
 def test_panels_store_rows_and_default_guess():
-    K, d = 40, 1234
+    K, d = 40, 1236                           # d % 4 == 0: the same float4 tile
     X, _ = _data(K, d, seed=5)
     P = bz().ClientPanels(K, d)
     for k in range(K):
         P.store(k, X[k])
     assert torch.equal(P.to_rows(), X)
     assert torch.equal(P.row(3), X[3])
-    a = bz().gm2(X, {"maxiter": 20, "guess": X.mean(dim=0)})
+    # (AUTO would take the register-resident kernel on the row-major input)
+    a = bz().gm2(X, {"maxiter": 20, "guess": X.mean(dim=0), "algo": "stream"})
     b = bz().gm2(P, {"maxiter": 20, "guess": X.mean(dim=0)})
     assert torch.equal(a, b)
     c = bz().gm2(P, {"maxiter": 20})          # guess = column mean of the panels

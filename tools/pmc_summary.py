@@ -14,11 +14,19 @@ import sys
 
 
 def per_kernel(path, counter):
+    """Mean counter value per launch over the WORK launches of each kernel: launches
+    under 1 % of the kernel's largest count are early exits (the lagged convergence
+    poll queues one pass past the stop; it returns at once) and are
+    left out of the mean, as the bench's HIP-event timing leaves them out."""
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
             acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
+    mean, n = {}, {}
+    for k, v in acc.items():
+        work = [x for x in v if x >= 0.01 * max(v)] or v
+        mean[k], n[k] = sum(work) / len(work), len(work)
+    return mean, n
 
 
 def main():
