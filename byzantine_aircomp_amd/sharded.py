@@ -24,6 +24,7 @@ import torch
 
 from . import _lib
 from .aggregators import GMResult, Context, _ALGO_NAMES, _ALGOS, _noise_source, _seed
+from .panels import ClientPanels
 
 __all__ = ["shard_range", "ShardedGM", "torch_allreduce_adapter"]
 
@@ -106,8 +107,12 @@ class ShardedGM:
         opts.update(options or {})
         if X.shape[1] != self.d_local or X.device != self.device or X.dtype != torch.float32:
             raise ValueError(f"X must be fp32 [K, {self.d_local}] on {self.device}")
-        if X.stride(1) != 1:
-            X = X.contiguous()
+        if isinstance(X, ClientPanels):      # this rank's columns in the panel layout
+            ptr, ldx, layout = X.data.data_ptr(), X.panel_stride, _lib.GM_LAYOUT_PANELS
+        else:
+            if X.stride(1) != 1:
+                X = X.contiguous()
+            ptr, ldx, layout = X.data_ptr(), max(X.stride(0), self.d_local), _lib.GM_LAYOUT_ROWS
         K = X.shape[0]
         guess = opts.get("guess")
         if guess is None:
@@ -120,6 +125,7 @@ class ShardedGM:
         o.eps = 1e-4
         o.mode = _lib.GM_MODE_AIRCOMP if aircomp else _lib.GM_MODE_IDEAL
         o.algo = _ALGOS[opts.get("algo", "auto")]
+        o.layout = layout
         if aircomp:
             var = opts["noise_var"]
             o.has_noise = int(var is not None)
@@ -133,7 +139,7 @@ class ShardedGM:
         res = _lib.GmResult()
         with torch.cuda.device(self.device):
             _lib.check(self.ctx.lib.gm_weiszfeld_f32(
-                self.ctx.handle, X.data_ptr(), K, self.d_local, max(X.stride(0), self.d_local),
+                self.ctx.handle, ptr, K, self.d_local, ldx,
                 g0.data_ptr(), out.data_ptr(), C.byref(o), C.byref(res),
                 torch.cuda.current_stream(self.device).cuda_stream), "gm_weiszfeld_f32")
         self.last_result = GMResult(res.iters, res.last_movement, bool(res.converged),
@@ -141,6 +147,7 @@ class ShardedGM:
         return out
 
     def gm2(self, X, options=None):
+        """X: this rank's [K, d_local] columns, as a tensor or a ClientPanels."""
         return self._run(X, options or {}, aircomp=False)
 
     def gm(self, X, options=None):

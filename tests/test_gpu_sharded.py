@@ -26,7 +26,7 @@ def _problem(K, d, B, seed):
     return X.cuda(), p.cuda()
 
 
-def _sharded(X, p, P, opts, aircomp, check_every=0, algo=0):
+def _sharded(X, p, P, opts, aircomp, check_every=0, algo=0, panels=False):
     from byzantine_aircomp_amd import _lib
     from byzantine_aircomp_amd.aggregators import Context
     from byzantine_aircomp_amd.sharded import _wrap, shard_range
@@ -55,16 +55,22 @@ def _sharded(X, p, P, opts, aircomp, check_every=0, algo=0):
                 torch.cuda.synchronize(dev)
             ctx.set_allreduce(allreduce)
             Xs = X[:, lo:hi].contiguous()
+            ptr, ldx = Xs.data_ptr(), hi - lo
+            if panels:
+                from byzantine_aircomp_amd import ClientPanels
+                Xs = ClientPanels.from_rows(Xs)
+                ptr, ldx = Xs.data.data_ptr(), Xs.panel_stride
             g0 = p[lo:hi].contiguous()
             res = torch.empty(hi - lo, device=dev)
             o = _lib.GmOpts()
             o.maxiter, o.tol, o.eps = opts["maxiter"], opts["tol"], 1e-4
             o.mode = _lib.GM_MODE_AIRCOMP if aircomp else _lib.GM_MODE_IDEAL
             o.check_every, o.algo = check_every, algo
+            o.layout = _lib.GM_LAYOUT_PANELS if panels else _lib.GM_LAYOUT_ROWS
             if aircomp:
                 o.has_noise, o.noise_var, o.P_max, o.seed = 1, opts["noise_var"], 1.0, opts["seed"]
             rr = _lib.GmResult()
-            _lib.check(ctx.lib.gm_weiszfeld_f32(ctx.handle, Xs.data_ptr(), K, hi - lo, hi - lo,
+            _lib.check(ctx.lib.gm_weiszfeld_f32(ctx.handle, ptr, K, hi - lo, ldx,
                                                 g0.data_ptr(), res.data_ptr(), C.byref(o),
                                                 C.byref(rr), None), "sharded gm")
             torch.cuda.synchronize(dev)
@@ -163,3 +169,26 @@ def test_sharded_gram_equals_unsharded(algo):
     if algo == 3:
         assert _sharded.algos == {_lib.GM_ALGO_GRAM}
     assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-5
+
+
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("check_every", [0, 1])
+def test_sharded_panels_equal_sharded_rows(P, check_every):
+    """Each rank's shard in the panel layout: the same chunks and reduction order
+    as the row-major shard (d_local % 4 == 0), so bit-identical results."""
+    X, p = _problem(1000, 40_960, 200, seed=20 + P)
+    opts = {"maxiter": 1000, "tol": 1e-5}
+    rows, it_r = _sharded(X, p, P, opts, aircomp=False, check_every=check_every, algo=1)
+    pan, it_p = _sharded(X, p, P, opts, aircomp=False, check_every=check_every, algo=1,
+                         panels=True)
+    assert it_r == it_p and len(it_p) == 1
+    assert torch.equal(rows, pan)
+
+
+def test_sharded_gm_panels_philox():
+    X, p = _problem(300, 8192, 60, seed=31)
+    opts = {"maxiter": 30, "tol": 1e-5, "noise_var": 1e-2, "seed": 77}
+    rows, _ = _sharded(X, p, 2, opts, aircomp=True, algo=1)
+    pan, it = _sharded(X, p, 2, opts, aircomp=True, algo=1, panels=True)
+    assert it == {30}
+    assert rel_l2(pan.cpu().numpy(), rows.cpu().numpy()) <= 1e-6
