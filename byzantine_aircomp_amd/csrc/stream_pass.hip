@@ -72,6 +72,8 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
     a.seed += (uint64_t)pb * kSeedStride;
   }
   if (!SUM_ONLY && a.st->done) return;
+  // INIT reads the guess per lane: as one dwordx4 when it is 16-byte aligned
+  const bool g_vec = V > 1 && (reinterpret_cast<uintptr_t>(a.g_old) & (4 * V - 1)) == 0;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -139,7 +141,14 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
     if constexpr (INIT) {
       const int64_t col = ch * J + (int64_t)c * V;
       const bool cval = ch < nch && col < d;
-      if (!PANEL || (ch + 1) * J <= d) {   // row-major: V | d, a lane's group is all-in or all-out
+      if (V > 1 && (ch + 1) * J <= d && g_vec) {   // full chunk, aligned guess: one load per lane
+        if constexpr (V > 1) {
+          typedef typename vec<V>::t GV;
+          const GV gv4 = *reinterpret_cast<const GV*>(a.g_old + col);
+#pragma unroll
+          for (int v = 0; v < V; ++v) t.g[v] = gv4[v];
+        }
+      } else if (!PANEL || (ch + 1) * J <= d) {   // row-major: V | d, groups all-in or all-out
 #pragma unroll
         for (int v = 0; v < V; ++v) t.g[v] = cval ? a.g_old[col + v] : 0.f;
       } else {                             // panels: d need not be a multiple of V
@@ -242,7 +251,13 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
       }
       e[i] = s;
       if constexpr (WANT_R) e2[i] = s2;
-      if constexpr (ROLL) fetch_row(nxt, t, i);
+      if constexpr (ROLL) {
+        // keep row i's next load behind row i's use: without the fence the
+        // compiler hoists all R loads above phase B (two live tiles, spills)
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" ::: "memory");
+        fetch_row(nxt, t, i);
+      }
     }
     if constexpr (ROLL) fetch_aux(nxt, t);
     transpose_reduce<LPR, R>(e, c);
