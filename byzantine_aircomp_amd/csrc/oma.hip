@@ -4,6 +4,8 @@
 // OMA:  X[k, j] += (h_re[k] * n_re[k, j] + h_im[k] * n_im[k, j]) / (h_re[k]^2 + h_im[k]^2)
 // One read + one write of X (8 B per element); the draws either come from the
 // caller (the reference's own CPU-generator values, bit-exact) or from Philox.
+#include <algorithm>
+
 #include "gmagg_internal.h"
 #include "philox.h"
 
@@ -29,22 +31,55 @@ __global__ void __launch_bounds__(256) oma_apply(float* __restrict__ X, int64_t 
   }
 }
 
-// Philox draws: h_k ~ CN(0, 1) per client, n_re/n_im ~ N(0, var) per element
-// keyed by the element's global index k * d_total + (col_off + j).
+// Philox draws (the production path: at C3 size one OMA call needs 2.2e10
+// normals).  Client k's channel h_k ~ CN(0, 1) is the Philox block keyed (row
+// k); element (k, global column c) takes n_re, n_im ~ N(0, var) = normals 2u,
+// 2u+1 (u = c & 1) of the block keyed (row k, pair c >> 1): one block serves
+// two elements, and a d-shard regenerates its own columns from its offset.
+// blockIdx.y walks rows (h_k and |h_k|^2 once per thread and row); a thread
+// owns groups of 4 columns (one float4 read + write when aligned).  Per element
+// ~1/2 Philox block + 1 Box-Muller pair, against 8 B of HBM traffic.
 __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t K, int64_t d,
-                                                  int64_t ldx, int64_t d_total, int64_t col_off,
-                                                  float sd, uint64_t seed) {
-  const int64_t n = K * d;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t k = e / d, j = e - k * d;
-    float h[4], z[4];
+                                                  int64_t ldx, int64_t col_off, float sd,
+                                                  uint64_t seed, int vec4) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const int64_t G = (d + 3) / 4;
+  for (int64_t k = blockIdx.y; k < K; k += gridDim.y) {
+    float h[4];
     normal4(seed, kStreamOmaChannel, 0, (uint64_t)k, h);
     const float a = h[0] * 0.70710678118654752f, b = h[1] * 0.70710678118654752f;
-    normal4(seed, kStreamOmaNoise, 0, (uint64_t)(k * d_total + col_off + j), z);
-    const float num = a * (sd * z[0]) + b * (sd * z[1]);
-    float* p = X + k * ldx + j;
-    *p = *p + num / (a * a + b * b);
+    const float den = a * a + b * b;
+    float* row = X + k * ldx;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G;
+         g += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t j0 = 4 * g;
+      const uint64_t c0 = (uint64_t)(col_off + j0);
+      const int sh = (int)(c0 & 1);                 // odd shard offsets span 3 pairs
+      float z[12];
+      normal4(seed, kStreamOmaNoise, (uint64_t)k, c0 >> 1, z);
+      normal4(seed, kStreamOmaNoise, (uint64_t)k, (c0 >> 1) + 1, z + 4);
+      if (sh) normal4(seed, kStreamOmaNoise, (uint64_t)k, (c0 >> 1) + 2, z + 8);
+      float add[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        // no contraction: the same rounding on every code path (the sh = 0 / 1
+        // variants were compiled with different FMA fusion: 1-ulp shard mismatches)
+#pragma clang fp contract(off)
+        const int q = 2 * (u + sh);
+        add[u] = (a * (sd * z[q]) + b * (sd * z[q + 1])) / den;
+      }
+      if (vec4 && j0 + 4 <= d) {
+        f4* p = reinterpret_cast<f4*>(row + j0);
+        f4 v = __builtin_nontemporal_load(p);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = v[u] + add[u];
+        __builtin_nontemporal_store(v, p);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (j0 + u < d) row[j0 + u] = row[j0 + u] + add[u];
+      }
+    }
   }
 }
 
@@ -104,8 +139,15 @@ hipError_t launch_oma_apply(float* X, int64_t K, int64_t d, int64_t ldx, const f
 
 hipError_t launch_oma_philox(float* X, int64_t K, int64_t d, int64_t ldx, int64_t d_total,
                              int64_t col_off, float sd, uint64_t seed, hipStream_t s) {
-  hipLaunchKernelGGL(oma_philox, dim3(grid_for(K * d)), dim3(256), 0, s, X, K, d, ldx, d_total,
-                     col_off, sd, seed);
+  (void)d_total;   // draws are keyed by (row, global column pair): no d_total needed
+  const int64_t G = (d + 3) / 4;
+  const int gy = (int)(K < 65535 ? K : 65535);
+  int64_t gx = (G + 255) / 256;
+  const int64_t cap = std::max<int64_t>(1, (8192 + gy - 1) / gy);   // ~8K blocks in flight
+  if (gx > cap) gx = cap;
+  const int vec4 = (reinterpret_cast<uintptr_t>(X) % 16 == 0) && ldx % 4 == 0;
+  hipLaunchKernelGGL(oma_philox, dim3((unsigned)gx, gy), dim3(256), 0, s, X, K, d, ldx, col_off,
+                     sd, seed, vec4);
   return hipGetLastError();
 }
 

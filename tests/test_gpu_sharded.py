@@ -192,3 +192,27 @@ def test_sharded_gm_panels_philox():
     pan, it = _sharded(X, p, 2, opts, aircomp=True, algo=1, panels=True)
     assert it == {30}
     assert rel_l2(pan.cpu().numpy(), rows.cpu().numpy()) <= 1e-6
+
+
+@pytest.mark.parametrize("cuts", [(0, 4096, 8192, 10_001), (0, 4097, 6000, 10_001)])
+def test_oma_philox_shard_invariant(cuts):
+    """OMA's Philox draws are keyed by (row, global column pair): a shard at any
+    column offset (even or odd, float4 or scalar path) regenerates exactly the
+    noise the unsharded call adds to its columns."""
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd.aggregators import Context
+    K, d = 7, 10_001
+    X = torch.randn(K, d, generator=torch.Generator().manual_seed(3)).cuda()
+    full = X.clone()
+    bz.OMA(full, 1e-2, seed=5)
+    assert not torch.equal(full, X)
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        ctx = Context(X.device.index)
+        ctx.set_shard(d, lo)
+        part = X[:, lo:hi].contiguous()
+        from byzantine_aircomp_amd import _lib
+        _lib.check(ctx.lib.gm_oma_philox_f32(ctx.handle, part.data_ptr(), K, hi - lo, hi - lo,
+                                             1e-2, 5, None), "oma shard")
+        torch.cuda.synchronize()
+        assert torch.equal(part, full[:, lo:hi]), (lo, hi)
+        ctx.close()
