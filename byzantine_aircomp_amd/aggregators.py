@@ -309,6 +309,20 @@ def Krum(wList, options):  # noqa: N802 - reference name (M:197)
 
 def OMA(message, noise_var=0.01, noise_source=None, seed=None):  # noqa: N802 - reference name
     """In-place per-client equalised AWGN (MNIST_Air_weight.py:385-394)."""
+    if isinstance(message, ClientPanels):
+        src = _noise_source({} if noise_source is None else {"noise_source": noise_source})
+        if src == _lib.GM_NOISE_HOST:          # the reference's [K, d] draws: via rows
+            rows = message.to_rows()
+            OMA(rows, noise_var, noise_source=noise_source, seed=seed)
+            message.copy_rows_(rows)
+            return message
+        ctx = context(message.device)
+        with torch.cuda.device(message.device):
+            _lib.check(ctx.lib.gm_oma_philox_panels_f32(
+                ctx.handle, message.data.data_ptr(), message.K, message.d, message.panel_stride,
+                float(noise_var), _seed({"seed": seed}), _stream_ptr(message.device)),
+                "gm_oma_philox_panels_f32")
+        return message
     if message.dtype != torch.float32:
         raise TypeError(f"OMA kernel is fp32 (got {message.dtype})")
     X = _stage(message)

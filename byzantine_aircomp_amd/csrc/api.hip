@@ -921,6 +921,22 @@ int gm_oma_philox_f32(gm_ctx* c, float* X, int64_t K, int64_t d, int64_t ldx, do
   return GM_OK;
 }
 
+int gm_oma_philox_panels_f32(gm_ctx* c, float* X, int64_t K, int64_t d, int64_t panel_stride,
+                             double noise_var, uint64_t seed, void* stream) {
+  const int64_t W = gm_panel_width(K);
+  if (!c || !X || K < 0 || d < 0 || noise_var < 0 || (K > 0 && W == 0) || panel_stride < K * W)
+    return fail(GM_ERR_INVALID, "gm_oma_philox_panels_f32: bad args");
+  if (K == 0 || d == 0) return GM_OK;
+  HIPCHK(hipSetDevice(c->device));
+  const int64_t d_total = c->d_total > 0 ? c->d_total : d;
+  const int64_t col_off = c->d_total > 0 ? c->d_offset : 0;
+  int wshift = 0;
+  while ((int64_t)1 << wshift < W) ++wshift;
+  HIPCHK(launch_oma_philox(X, K, d, panel_stride, d_total, col_off, (float)std::sqrt(noise_var),
+                           seed, reinterpret_cast<hipStream_t>(stream), wshift));
+  return GM_OK;
+}
+
 int gm_oma_apply_f32(gm_ctx* c, float* X, int64_t K, int64_t d, int64_t ldx, const float* hr,
                      const float* hi, const float* nr, const float* ni, void* stream) {
   if (!c || !X || !hr || !hi || !nr || !ni || K < 0 || d < 0 || ldx < d)

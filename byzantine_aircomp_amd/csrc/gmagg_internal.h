@@ -141,7 +141,8 @@ hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_
 hipError_t launch_oma_apply(float* X, int64_t K, int64_t d, int64_t ldx, const float* hr,
                             const float* hi, const float* nr, const float* ni, hipStream_t s);
 hipError_t launch_oma_philox(float* X, int64_t K, int64_t d, int64_t ldx, int64_t d_total,
-                             int64_t col_off, float sd, uint64_t seed, hipStream_t s);
+                             int64_t col_off, float sd, uint64_t seed, hipStream_t s,
+                             int wshift = 0);
 hipError_t launch_fill_clients(float* X, int64_t K, int64_t d, int64_t ldx, int64_t B,
                                float mu_h, float sd_h, float mu_b, float sd_b, int64_t d_total,
                                int64_t col_off, uint64_t seed, hipStream_t s);

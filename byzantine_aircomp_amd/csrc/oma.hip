@@ -39,9 +39,11 @@ __global__ void __launch_bounds__(256) oma_apply(float* __restrict__ X, int64_t 
 // blockIdx.y walks rows (h_k and |h_k|^2 once per thread and row); a thread
 // owns groups of 4 columns (one float4 read + write when aligned).  Per element
 // ~1/2 Philox block + 1 Box-Muller pair, against 8 B of HBM traffic.
+// wshift > 0: X is in the panel layout [ceil(d/W)][K][W], W = 1 << wshift, ldx = the
+// panel stride (elements); the draws are keyed the same way, so panels and rows agree.
 __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t K, int64_t d,
                                                   int64_t ldx, int64_t col_off, float sd,
-                                                  uint64_t seed, int vec4) {
+                                                  uint64_t seed, int vec4, int wshift) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   const int64_t G = (d + 3) / 4;
   for (int64_t k = blockIdx.y; k < K; k += gridDim.y) {
@@ -49,7 +51,7 @@ __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t
     normal4(seed, kStreamOmaChannel, 0, (uint64_t)k, h);
     const float a = h[0] * 0.70710678118654752f, b = h[1] * 0.70710678118654752f;
     const float den = a * a + b * b;
-    float* row = X + k * ldx;
+    float* row = wshift ? X + (k << wshift) : X + k * ldx;
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G;
          g += (int64_t)gridDim.x * blockDim.x) {
       const int64_t j0 = 4 * g;
@@ -68,8 +70,11 @@ __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t
         const int q = 2 * (u + sh);
         add[u] = (a * (sd * z[q]) + b * (sd * z[q + 1])) / den;
       }
+      // element j of this row: row[j] (rows), or panel j >> wshift, slot j & (W-1) (panels;
+      // W % 4 == 0, so a group of 4 never straddles panels)
+      float* rp = wshift ? row + (j0 >> wshift) * ldx + (j0 & ((1 << wshift) - 1)) - j0 : row;
       if (vec4 && j0 + 4 <= d) {
-        f4* p = reinterpret_cast<f4*>(row + j0);
+        f4* p = reinterpret_cast<f4*>(rp + j0);
         f4 v = __builtin_nontemporal_load(p);
 #pragma unroll
         for (int u = 0; u < 4; ++u) v[u] = v[u] + add[u];
@@ -77,7 +82,7 @@ __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t
       } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if (j0 + u < d) row[j0 + u] = row[j0 + u] + add[u];
+          if (j0 + u < d) rp[j0 + u] = rp[j0 + u] + add[u];
       }
     }
   }
@@ -138,7 +143,8 @@ hipError_t launch_oma_apply(float* X, int64_t K, int64_t d, int64_t ldx, const f
 }
 
 hipError_t launch_oma_philox(float* X, int64_t K, int64_t d, int64_t ldx, int64_t d_total,
-                             int64_t col_off, float sd, uint64_t seed, hipStream_t s) {
+                             int64_t col_off, float sd, uint64_t seed, hipStream_t s,
+                             int wshift) {
   (void)d_total;   // draws are keyed by (row, global column pair): no d_total needed
   const int64_t G = (d + 3) / 4;
   const int gy = (int)(K < 65535 ? K : 65535);
@@ -147,7 +153,7 @@ hipError_t launch_oma_philox(float* X, int64_t K, int64_t d, int64_t ldx, int64_
   if (gx > cap) gx = cap;
   const int vec4 = (reinterpret_cast<uintptr_t>(X) % 16 == 0) && ldx % 4 == 0;
   hipLaunchKernelGGL(oma_philox, dim3((unsigned)gx, gy), dim3(256), 0, s, X, K, d, ldx, col_off,
-                     sd, seed, vec4);
+                     sd, seed, vec4, wshift);
   return hipGetLastError();
 }
 

@@ -169,6 +169,12 @@ int gm_krum_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t ldx,
 int gm_oma_philox_f32(gm_ctx* ctx, float* X, int64_t K, int64_t d, int64_t ldx,
                       double noise_var, uint64_t seed, void* stream);
 
+/* The same OMA on client updates in the panel layout (GM_LAYOUT_PANELS: X as
+ * [ceil(d/W)][K][W], W = gm_panel_width(K), panel_stride >= K*W): identical draws
+ * and results to gm_oma_philox_f32 on the row-major matrix; padding untouched. */
+int gm_oma_philox_panels_f32(gm_ctx* ctx, float* X, int64_t K, int64_t d, int64_t panel_stride,
+                             double noise_var, uint64_t seed, void* stream);
+
 /* OMA with the reference's own draws (device arrays): h_re[K], h_im[K],
  * n_re[K*d], n_im[K*d] (row-major, already scaled by sqrt(noise_var)).
  * Bit-exact with the reference's fp32 op order. */

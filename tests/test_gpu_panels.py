@@ -97,3 +97,16 @@ def test_panels_reject_non_streaming_algos():
     for algo in ("gram", "twopass", "resident"):
         with pytest.raises(RuntimeError):
             bz().gm2(P, {"maxiter": 5, "guess": g0, "algo": algo})
+
+
+@pytest.mark.parametrize("K,d", [(50, 7850), (1000, 4099), (300, 257)])
+def test_oma_philox_on_panels_equals_rows(K, d):
+    """OMA's Philox draws are keyed by (client, global column): the panel kernel adds
+    exactly the noise the row-major kernel adds, and leaves the padding at zero."""
+    X, _ = _data(K, d, seed=11)
+    P = bz().ClientPanels.from_rows(X)
+    bz().OMA(X, 1e-2, seed=42)
+    bz().OMA(P, 1e-2, seed=42)
+    assert torch.equal(P.to_rows(), X)
+    if d % P.W:
+        assert torch.count_nonzero(P.data[-1, :, d % P.W:]) == 0
