@@ -870,7 +870,7 @@ int gm_mean_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, fl
 int gm_median_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, float* out,
                   void* stream) {
   if (!c || !X || !out || K < 1 || d < 0 || ldx < d) return fail(GM_ERR_INVALID, "gm_median_f32: bad args");
-  if (K > 256) return fail(GM_ERR_UNSUPPORTED, "gm_median_f32: K <= 256");
+  if (K > 2048) return fail(GM_ERR_UNSUPPORTED, "gm_median_f32: K <= 2048");
   if (d == 0) return GM_OK;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(launch_col_select(X, K, d, ldx, 0, 0, out, reinterpret_cast<hipStream_t>(stream)));
@@ -881,7 +881,7 @@ int gm_trimmed_mean_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t
                         int64_t trim, float* out, void* stream) {
   if (!c || !X || !out || K < 1 || d < 0 || ldx < d || trim < 0 || 2 * trim >= K)
     return fail(GM_ERR_INVALID, "gm_trimmed_mean_f32: bad args");
-  if (K > 256) return fail(GM_ERR_UNSUPPORTED, "gm_trimmed_mean_f32: K <= 256");
+  if (K > 2048) return fail(GM_ERR_UNSUPPORTED, "gm_trimmed_mean_f32: K <= 2048");
   if (d == 0) return GM_OK;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(launch_col_select(X, K, d, ldx, 1, trim, out, reinterpret_cast<hipStream_t>(stream)));
@@ -892,14 +892,16 @@ int gm_krum_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, in
                 float* out, int64_t* index, void* stream) {
   if (!c || !X || !out || K < 1 || d < 0 || ldx < d || honest < 2 || honest - 1 > K)
     return fail(GM_ERR_INVALID, "gm_krum_f32: bad args (needs 2 <= honestSize <= K+1)");
-  if (K > 1024) return fail(GM_ERR_UNSUPPORTED, "gm_krum_f32: K <= 1024");
+  if (K > 4096) return fail(GM_ERR_UNSUPPORTED, "gm_krum_f32: K <= 4096");
   HIPCHK(hipSetDevice(c->device));
   Workspace w;
-  int rc = ensure_ws(c, 1, 1, 1, &w, 0, (int)K);          // G area holds the K x K distances
+  // G area holds the K x K distances; the float slab holds the per-slice fp64 partials
+  const size_t part_doubles = (size_t)krum_slices(K, d) * (size_t)(K * K);
+  int rc = ensure_ws(c, K, 1, 1, &w, 2 * part_doubles, (int)K);
   if (rc) return rc;
-  int64_t* didx = reinterpret_cast<int64_t*>(w.sums);
-  HIPCHK(launch_krum(X, K, d, ldx, honest - 1, w.G, out, didx,
-                     reinterpret_cast<hipStream_t>(stream)));
+  int64_t* didx = reinterpret_cast<int64_t*>(w.u);
+  HIPCHK(launch_krum(X, K, d, ldx, honest - 1, w.G, reinterpret_cast<double*>(w.gslab), w.alpha,
+                     out, didx, reinterpret_cast<hipStream_t>(stream)));
   if (index) {
     HIPCHK(hipMemcpyAsync(index, didx, sizeof(int64_t), hipMemcpyDeviceToHost,
                           reinterpret_cast<hipStream_t>(stream)));

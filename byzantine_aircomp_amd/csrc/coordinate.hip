@@ -4,16 +4,14 @@
 //   median        M:194-195   lower median of each column (torch.median)
 //   Krum          M:197-204   the row with the smallest sum of squared distances to
 //                              its honestSize-1 nearest rows (itself included, M:200-201)
-// Column statistics stage a 64-column x K tile in LDS; selections rank each
-// element against its column with a stable tie-break (x_j < x_i, or x_j == x_i
-// and j < i), which gives torch's order statistics exactly for the median and
-// the trimmed set; sums are fp64, rounded once.
+// median / trimmed_mean select order statistics bit by bit (col_select below);
+// sums are fp64, rounded once.
+#include <algorithm>
+
 #include "device_util.h"
 #include "gmagg_internal.h"
 
 namespace gmk {
-
-constexpr int kColBlock = 64;     // columns per block (one per thread of wave 0.. )
 
 // mean: one thread per column, fp64 accumulation.
 __global__ void __launch_bounds__(256) col_mean(const float* __restrict__ X, int64_t K, int64_t d,
@@ -26,109 +24,341 @@ __global__ void __launch_bounds__(256) col_mean(const float* __restrict__ X, int
   }
 }
 
-// Order statistics over a 64-column tile in LDS.  mode 0: lower median;
-// mode 1: trimmed mean dropping b values at each end.
-template <int KMAX>
+// Order statistics by bit-wise selection on order-preserving keys.
+//
+// A column's K values live across one wave: lane l holds rows l, l+64, ...
+// (R = ceil(K/64) per lane).  Each float maps to a 32-bit key whose unsigned
+// order is the float order (negatives bit-inverted, positives with the sign bit
+// set; -0 folded onto +0; every NaN -> 0xFFFFFFFF, the largest key, as torch's
+// topk ranks NaN).  The r-th smallest key is built MSB-first: 32 steps, each
+// one v_cmp per held value and a scalar popcount of the ballot (the count is
+// wave-uniform, no cross-lane reduction).  That is 32·K/64 vector compares per
+// column instead of K^2 for pairwise ranking.  The value at a rank does not depend
+// on how ties are broken, so these are torch's order statistics exactly:
+//   median        r = (K-1)/2 (torch's lower median); any NaN in the column -> NaN
+//                 (torch.median propagates NaN);
+//   trimmed_mean  the sum of ranks b..K-b-1 = the values strictly between the two
+//                 selected keys + the ties at each end counted from the ballots,
+//                 summed in fp64 and rounded once.
+// Staging: a block loads a K x C tile (C columns, 4C-byte row segments) into LDS
+// with coalesced loads, then its 4 waves select C/4 columns each, reading the
+// column down the tile (row stride C+1 words: conflict-free).
+__device__ __forceinline__ uint32_t order_key(float x) {
+  uint32_t u = __float_as_uint(x);
+  if (x != x) return 0xFFFFFFFFu;
+  if (x == 0.f) u = 0u;
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_value(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// NC columns x NR ranks selected together: independent chains interleaved, so the
+// compare -> popcount -> decide latency of one chain hides behind the others.
+template <int R, int NC, int NR>
+__device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const int64_t (&r)[NR],
+                                             uint32_t (&ans)[NC][NR]) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int q = 0; q < NR; ++q) ans[c][q] = 0;
+  for (int bit = 31; bit >= 0; --bit) {
+    int64_t cnt[NC][NR];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        const uint32_t t = ans[c][q] | (1u << bit);
+        int64_t n = 0;
+#pragma unroll
+        for (int i = 0; i < R; ++i) n += __popcll(__ballot(key[c][i] < t));
+        cnt[c][q] = n;
+      }
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int q = 0; q < NR; ++q)
+        if (cnt[c][q] <= r[q]) ans[c][q] |= 1u << bit;
+  }
+}
+
+template <int R, int C>
 __global__ void __launch_bounds__(256) col_select(const float* __restrict__ X, int64_t K,
                                                   int64_t d, int64_t ldx, int mode, int64_t b,
-                                                  float* __restrict__ out) {
-  __shared__ float tile[KMAX][kColBlock + 1];
-  const int64_t j0 = (int64_t)blockIdx.x * kColBlock;
-  const int tc = threadIdx.x % kColBlock, tr = threadIdx.x / kColBlock;   // 4 row lanes
-  for (int64_t k = tr; k < K; k += blockDim.x / kColBlock)
-    tile[k][tc] = j0 + tc < d ? X[k * ldx + j0 + tc] : 0.f;
-  __syncthreads();
-  // 4 threads per column split the candidates i; combine through LDS.
-  __shared__ double acc[4][kColBlock];
-  __shared__ float med[4][kColBlock];
-  __shared__ int found[4][kColBlock];
-  const int64_t m = (K - 1) / 2;
-  double s = 0.0;
-  float mv = 0.f;
-  int fnd = 0;
-  for (int64_t i = tr; i < K; i += 4) {
-    const float xi = tile[i][tc];
-    int64_t rank = 0;
-    for (int64_t jj = 0; jj < K; ++jj) {
-      const float xj = tile[jj][tc];
-      rank += (xj < xi) || (xj == xi && jj < i);
-    }
-    if (mode == 0) {
-      if (rank == m) { mv = xi; fnd = 1; }
-    } else if (rank >= b && rank < K - b) {
-      s += (double)xi;
+                                                  int vec4, float* __restrict__ out) {
+  __shared__ float tile[64 * R][C + 1];
+  const int64_t ntiles = (d + C - 1) / C;
+  // XCD-aware: blocks bid and bid+8 run on the same XCD; give them adjacent tiles
+  // so the two halves of a 128-B line (C = 16) are fetched into one L2.
+  int64_t t = blockIdx.x;
+  if (C < 32 && t < ntiles / 16 * 16) t = t / 16 * 16 + (t % 8) * 2 + (t / 8) % 2;
+  const int64_t j0 = t * C;
+  {
+    // float4 per lane (LPR lanes per row segment), 16 loads in flight per thread
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    constexpr int LPR = C / 4, RPI = 256 / LPR;
+    const int tq = threadIdx.x % LPR, tr = threadIdx.x / LPR;
+    const int64_t col = j0 + 4 * tq;
+    const bool vec = vec4 && col + 4 <= d;
+    for (int64_t base = tr; base < K; base += 16 * RPI) {
+      f4 buf[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int64_t k = base + (int64_t)u * RPI;
+        buf[u] = f4{0.f, 0.f, 0.f, 0.f};
+        if (k < K) {
+          const float* src = X + k * ldx + col;
+          if (vec) {
+            buf[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src));
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) buf[u][e] = col + e < d ? src[e] : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int64_t k = base + (int64_t)u * RPI;
+        if (k < K) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) tile[k][4 * tq + e] = buf[u][e];
+        }
+      }
     }
   }
-  acc[tr][tc] = s;
-  med[tr][tc] = mv;
-  found[tr][tc] = fnd;
   __syncthreads();
-  if (tr == 0 && j0 + tc < d) {
+  // wave w selects columns w, w+4, ... in pairs (w + 8m, w + 8m + 4): C % 8 == 0
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int c0 = w; c0 < C; c0 += 8) {
+    if (j0 + c0 >= d) break;
+    uint32_t key[2][R];      // values are recovered from keys (key_value) when summed
+    bool nan[2] = {false, false};
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int row = lane + 64 * i;
+        const bool ok = row < K && j0 + c0 + 4 * h < d;
+        const float x = ok ? tile[row][c0 + 4 * h] : 0.f;
+        key[h][i] = ok ? order_key(x) : 0xFFFFFFFFu;
+        nan[h] |= ok && x != x;
+      }
+    float res[2];
     if (mode == 0) {
-      float v = 0.f;
-      for (int r = 0; r < 4; ++r)
-        if (found[r][tc]) v = med[r][tc];
-      out[j0 + tc] = v;
+      const int64_t rk[1] = {(K - 1) / 2};
+      uint32_t ans[2][1];
+      select_ranks<R, 2, 1>(key, rk, ans);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        res[h] = __ballot(nan[h]) ? __uint_as_float(0x7FC00000u) : key_value(ans[h][0]);
     } else {
-      double t = 0.0;
-      for (int r = 0; r < 4; ++r) t += acc[r][tc];
-      out[j0 + tc] = (float)(t / (double)(K - 2 * b));
+      const int64_t rk[2] = {b, K - b - 1};
+      uint32_t ans[2][2];
+      select_ranks<R, 2, 2>(key, rk, ans);
+      const int64_t n = K - 2 * b;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t lo = ans[h][0], hi = ans[h][1];
+        const float vlo = key_value(lo), vhi = key_value(hi);
+        double sum;
+        if (lo == hi) {
+          sum = (double)n * (double)vlo;
+        } else {
+          double sv = 0.0;
+          int64_t le_lo = 0, lt_hi = 0;
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            if (key[h][i] > lo && key[h][i] < hi) sv += (double)key_value(key[h][i]);
+            le_lo += __popcll(__ballot(key[h][i] <= lo));
+            lt_hi += __popcll(__ballot(key[h][i] < hi));
+          }
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) sv += __shfl_xor(sv, o);
+          sum = sv + (double)(le_lo - b) * (double)vlo + (double)((K - b) - lt_hi) * (double)vhi;
+        }
+        res[h] = (float)(sum / (double)n);
+      }
+    }
+    if (lane == 0) {
+      out[j0 + c0] = res[0];
+      if (j0 + c0 + 4 < d) out[j0 + c0 + 4] = res[1];
     }
   }
 }
 
-// Krum, step 1: squared distance of every row pair (i <= j), one block per pair,
-// fp32 squared differences accumulated in fp64 (M:199 sums over d in fp32).
-__global__ void __launch_bounds__(256) pair_dist(const float* __restrict__ X, int64_t K, int64_t d,
-                                                 int64_t ldx, double* __restrict__ D) {
-  __shared__ double scratch[16];
-  const int64_t p = blockIdx.x;
-  // decode p -> (i, j), i <= j, row-major over the upper triangle
-  int64_t i = 0, rem = p;
-  while (rem >= K - i) { rem -= K - i; ++i; }
-  const int64_t j = i + rem;
+// Krum, step 1: squared distances of every row pair, register-tiled.
+// A block owns a 128 x 128 tile of pairs (row tiles bi <= bj: D is symmetric)
+// over one slice of the columns; each thread an 8 x 8 sub-tile.  Per 32-column
+// stage both row tiles go to LDS column-major (sA[c][r]), so a thread reads its
+// 8 rows of one column as two ds_read_b128 and does 64 (sub, fma) pairs: the
+// exact differences of M:199 in fp32, squares summed in fp32 over the stage and
+// in fp64 across stages.  Slices write fp64 partials [S][K][K]; pair_reduce sums
+// them in a fixed order (deterministic, no atomics).
+constexpr int kPT = 128;   // pair-tile edge (rows)
+constexpr int kPC = 32;    // columns per LDS stage
+
+template <bool VEC>
+__global__ void __launch_bounds__(256) pair_dist(const float* __restrict__ X, int64_t K,
+                                                 int64_t d, int64_t ldx, int64_t chunk,
+                                                 double* __restrict__ part) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) float sA[kPC][kPT + 4];
+  __shared__ __attribute__((aligned(16))) float sB[kPC][kPT + 4];
+  const int64_t nT = (K + kPT - 1) / kPT;
+  int64_t p = blockIdx.x, bi = 0;
+  while (p >= nT - bi) { p -= nT - bi; ++bi; }
+  const int64_t bj = bi + p;
+  const int64_t cb = (int64_t)blockIdx.y * chunk, ce = cb + chunk < d ? cb + chunk : d;
+  const int ti = threadIdx.x >> 4, tj = threadIdx.x & 15;
+  double accd[8][8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int v = 0; v < 8; ++v) accd[u][v] = 0.0;
+  // stage loads: thread owns (row r, columns cg..cg+3) of both row tiles for q = 0..3;
+  // the next stage's loads are issued before this stage's arithmetic (register prefetch)
+  f4 pre[4][2];
+  auto load_stage = [&](int64_t c0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = threadIdx.x + 256 * q, r = idx >> 3, cg = (idx & 7) * 4;
+      const int64_t col = c0 + cg;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int64_t row = (t ? bj : bi) * kPT + r;
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (row < K && col < ce) {
+          const float* src = X + row * ldx + col;
+          if (VEC && col + 4 <= ce) {
+            v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src));
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = col + u < ce ? src[u] : 0.f;
+          }
+        }
+        pre[q][t] = v;
+      }
+    }
+  };
+  if (cb < ce) load_stage(cb);
+  for (int64_t c0 = cb; c0 < ce; c0 += kPC) {
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = threadIdx.x + 256 * q, r = idx >> 3, cg = (idx & 7) * 4;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        sA[cg + u][r] = pre[q][0][u];
+        sB[cg + u][r] = pre[q][1][u];
+      }
+    }
+    __syncthreads();
+    if (c0 + kPC < ce) load_stage(c0 + kPC);
+    float acc[8][8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int v = 0; v < 8; ++v) acc[u][v] = 0.f;
+#pragma unroll 4
+    for (int c = 0; c < kPC; ++c) {
+      const f4 a0 = *reinterpret_cast<const f4*>(&sA[c][ti * 8]);
+      const f4 a1 = *reinterpret_cast<const f4*>(&sA[c][ti * 8 + 4]);
+      const f4 b0 = *reinterpret_cast<const f4*>(&sB[c][tj * 8]);
+      const f4 b1 = *reinterpret_cast<const f4*>(&sB[c][tj * 8 + 4]);
+      const float a[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      const float b[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+          const float t = a[u] - b[v];
+          acc[u][v] = fmaf(t, t, acc[u][v]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int v = 0; v < 8; ++v) accd[u][v] += (double)acc[u][v];
+  }
+  double* P = part + (int64_t)blockIdx.y * K * K;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int64_t i = bi * kPT + ti * 8 + u;
+    if (i >= K) break;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const int64_t j = bj * kPT + tj * 8 + v;
+      if (j < K) P[i * K + j] = accd[u][v];
+    }
+  }
+}
+
+// D[i][j] (i <= j: the tile of (i, j) has bi <= bj, so it was computed) = the sum
+// over slices in slice order; one wave per 64 consecutive elements, 4 waves split
+// the slices and combine in a fixed order (deterministic, no atomics).
+__global__ void __launch_bounds__(256) pair_reduce(const double* __restrict__ part, int64_t S,
+                                                   int64_t K, double* __restrict__ D) {
+  __shared__ double red[4][64];
+  const int64_t n = K * K;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t i = e / K, j = e - i * K;
+  const bool on = e < n && i <= j;
+  const int64_t s0 = S * w / 4, s1 = S * (w + 1) / 4;
   double s = 0.0;
-  const float* a = X + i * ldx;
-  const float* bb = X + j * ldx;
-  for (int64_t c = threadIdx.x; c < d; c += blockDim.x) {
-    const float t = a[c] - bb[c];
-    s += (double)(t * t);
+  if (on) {
+#pragma unroll 8
+    for (int64_t t = s0; t < s1; ++t) s += part[t * n + e];
   }
-  s = block_sum(s, scratch);
-  if (threadIdx.x == 0) {
-    D[i * K + j] = s;
-    D[j * K + i] = s;
-  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && on) D[e] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
-// Krum, step 2 (one block): score_i = sum of the kk smallest D[i][*] (self included),
-// index = first argmin (torch.argmin), out = that row.
-__global__ void __launch_bounds__(256) krum_select(const double* __restrict__ D, int64_t K,
-                                                   int64_t kk, const float* __restrict__ X,
-                                                   int64_t d, int64_t ldx, float* __restrict__ out,
-                                                   int64_t* index) {
-  __shared__ double score[1024];
-  __shared__ int64_t s_best;
-  for (int64_t i = threadIdx.x; i < K; i += blockDim.x) {
-    const double* row = D + i * K;
-    double sc = 0.0;
-    for (int64_t jj = 0; jj < K; ++jj) {          // stable rank of D[i][jj] in its row
-      int64_t rank = 0;
-      for (int64_t t = 0; t < K; ++t) rank += (row[t] < row[jj]) || (row[t] == row[jj] && t < jj);
-      if (rank < kk) sc += row[jj];
-    }
-    score[i] = sc;
-  }
+// Krum, step 2 (one block per row): score_i = sum of the kk smallest D[i][*] (self
+// included, M:200-201), by stable rank over the row staged in LDS.
+__global__ void __launch_bounds__(256) krum_score(const double* __restrict__ D, int64_t K,
+                                                  int64_t kk, double* __restrict__ score) {
+  extern __shared__ double srow[];
+  __shared__ double scratch[8];
+  const int64_t i = blockIdx.x;
+  for (int64_t j = threadIdx.x; j < K; j += blockDim.x) srow[j] = D[i <= j ? i * K + j : j * K + i];
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int64_t best = 0;
-    for (int64_t i = 1; i < K; ++i)
-      if (score[i] < score[best]) best = i;
-    s_best = best;
-    if (index) *index = best;
+  double sc = 0.0;
+  for (int64_t j = threadIdx.x; j < K; j += blockDim.x) {
+    const double x = srow[j];
+    int64_t rank = 0;
+    for (int64_t t = 0; t < K; ++t) rank += (srow[t] < x) || (srow[t] == x && t < j);
+    if (rank < kk) sc += x;
   }
-  __syncthreads();
-  for (int64_t c = threadIdx.x; c < d; c += blockDim.x) out[c] = X[s_best * ldx + c];
+  sc = block_sum(sc, scratch);
+  if (threadIdx.x == 0) score[i] = sc;
+}
+
+// Krum, step 3: index = first argmin of the scores (torch.argmin), one wave.
+__global__ void __launch_bounds__(64) krum_argmin(const double* __restrict__ score, int64_t K,
+                                                  int64_t* __restrict__ index) {
+  int64_t best = -1;
+  double bv = 0.0;
+  for (int64_t i = threadIdx.x; i < K; i += 64)
+    if (best < 0 || score[i] < bv) { bv = score[i]; best = i; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(bv, o);
+    const int64_t oi = __shfl_xor(best, o);
+    if (oi >= 0 && (best < 0 || ov < bv || (ov == bv && oi < best))) { bv = ov; best = oi; }
+  }
+  if (threadIdx.x == 0) *index = best;
+}
+
+// Krum, step 4: out = row *index, grid-wide copy.
+__global__ void __launch_bounds__(256) copy_row(const float* __restrict__ X, int64_t d,
+                                                int64_t ldx, const int64_t* __restrict__ index,
+                                                float* __restrict__ out) {
+  const float* src = X + *index * ldx;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < d;
+       c += (int64_t)gridDim.x * blockDim.x)
+    out[c] = src[c];
 }
 
 static int grid_cols(int64_t d) {
@@ -144,24 +374,72 @@ hipError_t launch_col_mean(const float* X, int64_t K, int64_t d, int64_t ldx, fl
 
 hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, int mode,
                              int64_t b, float* out, hipStream_t s) {
-  const dim3 grid((unsigned)((d + kColBlock - 1) / kColBlock));
-  if (K <= 64)
-    hipLaunchKernelGGL(col_select<64>, grid, dim3(256), 0, s, X, K, d, ldx, mode, b, out);
-  else if (K <= 256)
-    hipLaunchKernelGGL(col_select<256>, grid, dim3(256), 0, s, X, K, d, ldx, mode, b, out);
-  else
-    return hipErrorInvalidValue;
+  const int vec4 = reinterpret_cast<uintptr_t>(X) % 16 == 0 && ldx % 4 == 0;
+#define GMK_SEL(R, C)                                                                       \
+  hipLaunchKernelGGL((col_select<R, C>), dim3((unsigned)((d + C - 1) / C)), dim3(256), 0, s, X, K, \
+                     d, ldx, mode, b, vec4, out)
+  if (K <= 64) GMK_SEL(1, 32);
+  else if (K <= 128) GMK_SEL(2, 32);
+  else if (K <= 256) GMK_SEL(4, 32);
+  else if (K <= 512) GMK_SEL(8, 16);
+  else if (K <= 1024) GMK_SEL(16, 16);
+  else if (K <= 2048) GMK_SEL(32, 8);
+  else return hipErrorInvalidValue;
+#undef GMK_SEL
   return hipGetLastError();
 }
 
+// Column slices for pair_dist: the block count pairs * S is chosen so the grid fills
+// whole rounds of co-resident blocks (time ~ rounds / S), partials <= 512 MiB.
+int64_t krum_slices(int64_t K, int64_t d) {
+  static int per_round = 0;                          // co-resident pair_dist blocks
+  if (!per_round) {
+    int dev = 0, cus = 256, occ = 1;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pair_dist<true>, 256, 0) != hipSuccess ||
+        occ < 1)
+      occ = 1;
+    per_round = cus * occ;
+  }
+  const int64_t nT = (K + kPT - 1) / kPT, pairs = nT * (nT + 1) / 2;
+  int64_t smax = (int64_t)(512ull << 20) / (8 * K * K);
+  const int64_t stages = (d + kPC - 1) / kPC;
+  if (smax > stages) smax = stages;
+  if (smax > 4 * (int64_t)per_round) smax = 4 * (int64_t)per_round;
+  if (smax < 1) return 1;
+  int64_t best = 1;
+  double best_cost = 1e300;
+  for (int64_t S = 1; S <= smax; ++S) {
+    const double cost = (double)((pairs * S + per_round - 1) / per_round) / (double)S;
+    if (cost < best_cost * (1 - 1e-9)) { best_cost = cost; best = S; }
+  }
+  return best;
+}
+
 hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t kk, double* D,
-                       float* out, int64_t* index, hipStream_t s) {
-  if (K > 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pair_dist, dim3((unsigned)(K * (K + 1) / 2)), dim3(256), 0, s, X, K, d, ldx,
-                     D);
+                       double* part, double* score, float* out, int64_t* index, hipStream_t s) {
+  const int64_t nT = (K + kPT - 1) / kPT, pairs = nT * (nT + 1) / 2;
+  const int64_t S = krum_slices(K, d);
+  const int64_t chunk = ((d + S - 1) / S + kPC - 1) / kPC * kPC;
+  const bool vec = reinterpret_cast<uintptr_t>(X) % 16 == 0 && ldx % 4 == 0;
+  if (vec)
+    hipLaunchKernelGGL(pair_dist<true>, dim3((unsigned)pairs, (unsigned)S), dim3(256), 0, s, X, K,
+                       d, ldx, chunk, part);
+  else
+    hipLaunchKernelGGL(pair_dist<false>, dim3((unsigned)pairs, (unsigned)S), dim3(256), 0, s, X,
+                       K, d, ldx, chunk, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(krum_select, dim3(1), dim3(256), 0, s, D, K, kk, X, d, ldx, out, index);
+  hipLaunchKernelGGL(pair_reduce, dim3((unsigned)((K * K + 63) / 64)), dim3(256), 0, s, part, S, K,
+                     D);
+  hipLaunchKernelGGL(krum_score, dim3((unsigned)K), dim3(256), sizeof(double) * K, s, D, K, kk,
+                     score);
+  hipLaunchKernelGGL(krum_argmin, dim3(1), dim3(64), 0, s, score, K, index);
+  if (d > 0)
+    hipLaunchKernelGGL(copy_row, dim3((unsigned)std::min<int64_t>((d + 255) / 256, 2048)),
+                       dim3(256), 0, s, X, d, ldx, index, out);
   return hipGetLastError();
 }
 

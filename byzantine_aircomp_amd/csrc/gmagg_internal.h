@@ -134,8 +134,10 @@ hipError_t launch_col_mean(const float* X, int64_t K, int64_t d, int64_t ldx, fl
                            hipStream_t s);
 hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, int mode,
                              int64_t b, float* out, hipStream_t s);
+// Krum: D [K][K] fp64, part [krum_slices(K, d)][K][K] fp64, score [K] fp64.
+int64_t krum_slices(int64_t K, int64_t d);
 hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t kk, double* D,
-                       float* out, int64_t* index, hipStream_t s);
+                       double* part, double* score, float* out, int64_t* index, hipStream_t s);
 
 // OMA / synthetic fills (oma.hip).
 hipError_t launch_oma_apply(float* X, int64_t K, int64_t d, int64_t ldx, const float* hr,

@@ -31,58 +31,68 @@ __global__ void __launch_bounds__(256) oma_apply(float* __restrict__ X, int64_t 
   }
 }
 
-// Philox draws (the production path: at C3 size one OMA call needs 2.2e10
-// normals).  Client k's channel h_k ~ CN(0, 1) is the Philox block keyed (row
-// k); element (k, global column c) takes n_re, n_im ~ N(0, var) = normals 2u,
-// 2u+1 (u = c & 1) of the block keyed (row k, pair c >> 1): one block serves
-// two elements, and a d-shard regenerates its own columns from its offset.
-// blockIdx.y walks rows (h_k and |h_k|^2 once per thread and row); a thread
-// owns groups of 4 columns (one float4 read + write when aligned).  Per element
-// ~1/2 Philox block + 1 Box-Muller pair, against 8 B of HBM traffic.
+// Philox draws (the production path: at C3 size one OMA call adds 1.1e10 noise
+// values).  The reference adds (h_re n_re + h_im n_im) / |h|^2 with n_re, n_im ~
+// N(0, var) independent (M:389-394): a sum of independent zero-mean normals, i.e.
+// exactly N(0, var |h|^2) / |h|^2 = N(0, var / |h|^2).  So one standard normal z per
+// element suffices: X += (sd / |h_k|) z, the same distribution as the reference's
+// two draws at half the random numbers.  Client k's channel h_k ~ CN(0, 1) is the
+// Philox block keyed (row k); element (k, global column c) takes normal c & 3 of
+// the block keyed (row k, c >> 2): one Philox block and two Box-Muller pairs per 4
+// elements, and a d-shard regenerates its own columns from its offset.
+// blockIdx.y walks rows (the row scale once per thread and row); a thread owns
+// groups of 4 columns (one float4 read + write when aligned).
 // wshift > 0: X is in the panel layout [ceil(d/W)][K][W], W = 1 << wshift, ldx = the
 // panel stride (elements); the draws are keyed the same way, so panels and rows agree.
 __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t K, int64_t d,
                                                   int64_t ldx, int64_t col_off, float sd,
                                                   uint64_t seed, int vec4, int wshift) {
   typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int U = 4;                        // groups per thread per step: 4 loads in flight
   const int64_t G = (d + 3) / 4;
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
   for (int64_t k = blockIdx.y; k < K; k += gridDim.y) {
     float h[4];
-    normal4(seed, kStreamOmaChannel, 0, (uint64_t)k, h);
+    normal4_hw(seed, kStreamOmaChannel, 0, (uint64_t)k, h);
     const float a = h[0] * 0.70710678118654752f, b = h[1] * 0.70710678118654752f;
-    const float den = a * a + b * b;
+    const float scale = sd / sqrtf(a * a + b * b);
     float* row = wshift ? X + (k << wshift) : X + k * ldx;
-    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G;
-         g += (int64_t)gridDim.x * blockDim.x) {
-      const int64_t j0 = 4 * g;
-      const uint64_t c0 = (uint64_t)(col_off + j0);
-      const int sh = (int)(c0 & 1);                 // odd shard offsets span 3 pairs
-      float z[12];
-      normal4(seed, kStreamOmaNoise, (uint64_t)k, c0 >> 1, z);
-      normal4(seed, kStreamOmaNoise, (uint64_t)k, (c0 >> 1) + 1, z + 4);
-      if (sh) normal4(seed, kStreamOmaNoise, (uint64_t)k, (c0 >> 1) + 2, z + 8);
-      float add[4];
+    for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g0 < G; g0 += U * T) {
+      // the loads go out before the Philox math so their latency hides behind it
+      f4 v[U];
+      float* rp[U];
+      bool full[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        // no contraction: the same rounding on every code path (the sh = 0 / 1
-        // variants were compiled with different FMA fusion: 1-ulp shard mismatches)
-#pragma clang fp contract(off)
-        const int q = 2 * (u + sh);
-        add[u] = (a * (sd * z[q]) + b * (sd * z[q + 1])) / den;
+      for (int q = 0; q < U; ++q) {
+        const int64_t j0 = 4 * (g0 + q * T);
+        // element j of this row: row[j] (rows), or panel j >> wshift, slot j & (W-1)
+        // (panels; W % 4 == 0, so a group of 4 never straddles panels)
+        rp[q] = wshift ? row + (j0 >> wshift) * ldx + (j0 & ((1 << wshift) - 1)) - j0 : row;
+        full[q] = vec4 && j0 + 4 <= d;
+        v[q] = f4{0.f, 0.f, 0.f, 0.f};
+        if (full[q]) v[q] = __builtin_nontemporal_load(reinterpret_cast<f4*>(rp[q] + j0));
       }
-      // element j of this row: row[j] (rows), or panel j >> wshift, slot j & (W-1) (panels;
-      // W % 4 == 0, so a group of 4 never straddles panels)
-      float* rp = wshift ? row + (j0 >> wshift) * ldx + (j0 & ((1 << wshift) - 1)) - j0 : row;
-      if (vec4 && j0 + 4 <= d) {
-        f4* p = reinterpret_cast<f4*>(rp + j0);
-        f4 v = __builtin_nontemporal_load(p);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = v[u] + add[u];
-        __builtin_nontemporal_store(v, p);
-      } else {
+      for (int q = 0; q < U; ++q) {
+        const int64_t j0 = 4 * (g0 + q * T);
+        if (j0 >= d) break;
+        const uint64_t c0 = (uint64_t)(col_off + j0);
+        const int sh = (int)(c0 & 3);               // unaligned shard offsets span 2 blocks
+        float z[8];
+        normal4_hw(seed, kStreamOmaNoise, (uint64_t)k, c0 >> 2, z);
+        if (sh) normal4_hw(seed, kStreamOmaNoise, (uint64_t)k, (c0 >> 2) + 1, z + 4);
+        float add[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (j0 + u < d) rp[j0 + u] = rp[j0 + u] + add[u];
+        for (int u = 0; u < 4; ++u) add[u] = scale * z[u + sh];
+        if (full[q]) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[q][u] = v[q][u] + add[u];
+          __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(rp[q] + j0));
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (j0 + u < d) rp[q][j0 + u] = rp[q][j0 + u] + add[u];
+        }
       }
     }
   }
@@ -145,7 +155,7 @@ hipError_t launch_oma_apply(float* X, int64_t K, int64_t d, int64_t ldx, const f
 hipError_t launch_oma_philox(float* X, int64_t K, int64_t d, int64_t ldx, int64_t d_total,
                              int64_t col_off, float sd, uint64_t seed, hipStream_t s,
                              int wshift) {
-  (void)d_total;   // draws are keyed by (row, global column pair): no d_total needed
+  (void)d_total;   // draws are keyed by (row, global column quad): no d_total needed
   const int64_t G = (d + 3) / 4;
   const int gy = (int)(K < 65535 ? K : 65535);
   int64_t gx = (G + 255) / 256;

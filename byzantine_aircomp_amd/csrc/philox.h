@@ -68,6 +68,27 @@ __host__ __device__ __forceinline__ void normal4(uint64_t seed, uint32_t stream,
   box_muller(r.z, r.w, &out[2], &out[3]);
 }
 
+// Box-Muller on the hardware transcendentals: v_log_f32 (log2), v_sqrt_f32 and
+// v_sin/v_cos_f32, which take their argument in revolutions, so u01(b) goes in
+// unscaled.  ~1 ulp each; contraction off so every call site rounds alike (a
+// normal must come out identical whichever code path regenerates it).
+__device__ __forceinline__ void box_muller_hw(uint32_t a, uint32_t b, float* n0, float* n1) {
+#pragma clang fp contract(off)
+  const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01(a)));
+  const float t = u01(b);
+  *n0 = r * __builtin_amdgcn_cosf(t);
+  *n1 = r * __builtin_amdgcn_sinf(t);
+}
+
+// normal4 with the hardware Box-Muller (the OMA production path).
+__device__ __forceinline__ void normal4_hw(uint64_t seed, uint32_t stream, uint64_t iter,
+                                           uint64_t idx, float out[4]) {
+  u4 c{(uint32_t)idx, (uint32_t)(idx >> 32), (uint32_t)iter, stream ^ (uint32_t)(iter >> 32)};
+  u4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  box_muller_hw(r.x, r.y, &out[0], &out[1]);
+  box_muller_hw(r.z, r.w, &out[2], &out[3]);
+}
+
 // One standard normal for element `idx` (uses half of a Philox block).
 __host__ __device__ __forceinline__ float normal1(uint64_t seed, uint32_t stream, uint64_t iter,
                                                   uint64_t idx) {

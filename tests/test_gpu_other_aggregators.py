@@ -50,3 +50,65 @@ def test_other_aggregators_cpu_input_roundtrip():
     X = torch.randn(11, 99)
     assert bz.median(X).device.type == "cpu"
     assert torch.equal(bz.median(X), orc.median(X))
+
+
+@pytest.mark.parametrize("K,d", [(129, 77), (300, 513), (513, 130), (1000, 200), (1025, 33),
+                                 (2048, 17)])
+def test_coordinate_aggregators_large_K(K, d):
+    """Bit-wise selection at every LDS tile shape (K up to 2048), ties included."""
+    import byzantine_aircomp_amd as bz
+    g = torch.Generator().manual_seed(K * 7 + d)
+    X = torch.randn(K, d, generator=g)
+    X[:, ::5] = torch.round(4 * X[:, ::5]) / 4        # heavy ties
+    X[:, 3] = 1.5                                      # a constant column
+    Xc = X.cuda()
+    assert np.array_equal(bz.median(Xc).cpu().numpy(), orc.median(X).numpy())
+    assert rel_l2(bz.trimmed_mean(Xc).cpu().numpy(), orc.trimmed_mean(X).numpy()) <= 1e-6
+
+
+def test_coordinate_aggregators_special_values():
+    """torch semantics: median propagates NaN; topk ranks NaN above +inf, so a NaN in
+    the trimmed top b is dropped and one in the middle makes the mean NaN; -0 == +0."""
+    import byzantine_aircomp_amd as bz
+    K, d = 20, 9
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(K, d, generator=g)
+    X[0, 0] = float("nan")                             # one NaN: trimmed (top 2) drops it
+    X[:3, 1] = float("nan")                            # three NaNs: one reaches the middle
+    X[:, 2] = 0.0
+    X[::2, 2] = -0.0
+    X[0, 3], X[1, 3] = float("inf"), float("-inf")
+    X[:, 4] = -X[:, 4].abs()                           # all negative
+    Xc = X.cuda()
+    m = bz.median(Xc).cpu()
+    want = orc.median(X)
+    assert torch.equal(torch.isnan(m), torch.isnan(want))
+    ok = ~torch.isnan(want)
+    assert torch.equal(m[ok], want[ok])
+    t = bz.trimmed_mean(Xc).cpu()
+    tw = orc.trimmed_mean(X)
+    assert torch.equal(torch.isnan(t), torch.isnan(tw))
+    ok = ~torch.isnan(tw)
+    assert rel_l2(t[ok].numpy(), tw[ok].numpy()) <= 1e-6
+
+
+@pytest.mark.parametrize("K,d,honest", [(129, 1001, 100), (300, 4096, 240), (260, 77, 200)])
+def test_krum_multi_tile_vs_oracle(K, d, honest):
+    """Pair tiles of 128 rows: K spanning 2-3 row tiles, ragged d (scalar column tail)."""
+    import byzantine_aircomp_amd as bz
+    g = torch.Generator().manual_seed(K + d + honest)
+    X = 0.05 * torch.randn(K, d, generator=g)
+    X[honest:] += 0.5 * torch.randn(K - honest, d, generator=g)
+    perm = torch.randperm(K, generator=g)            # Byzantine rows anywhere
+    X = X[perm].contiguous()
+    out = bz.Krum(X.cuda(), {"honestSize": honest})
+    assert torch.equal(out.cpu(), orc.krum(X, {"honestSize": honest}))
+
+
+def test_krum_strided_rows():
+    import byzantine_aircomp_amd as bz
+    g = torch.Generator().manual_seed(9)
+    base = torch.randn(40, 530, generator=g)
+    X = base[:, 3:520]                                # ldx = 530, unaligned start
+    out = bz.Krum(X.cuda(), {"honestSize": 30})
+    assert torch.equal(out.cpu(), orc.krum(X.contiguous(), {"honestSize": 30}))

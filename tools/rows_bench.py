@@ -96,17 +96,30 @@ def main():
                                  ("trimmed_mean", bz.trimmed_mean, 4.0 * K * d)):
             t = timed(lambda: fn(X, {}))
             emit({"row": "f3", "what": name, "K": K, "d": d, "ms": t * 1e3, "bytes": nbytes,
-                  "hbm_frac": nbytes / t / HBM,
-                  "compares_per_s": (K * K * d / t) if name != "mean" else None})
+                  "hbm_frac": nbytes / t / HBM})
         Kk, dk = 256, 262_144
         Xk = X[:, :dk].contiguous()
-        t = timed(lambda: bz.Krum(Xk, {"honestSize": 205}), reps=1, warm=1)
+        t = timed(lambda: bz.Krum(Xk, {"honestSize": 205}), reps=3, warm=1)
         pairs = Kk * (Kk + 1) / 2
         emit({"row": "f3", "what": "Krum", "K": Kk, "d": dk, "ms": t * 1e3,
-              "flops": 3.0 * pairs * dk, "bytes_min": 4.0 * Kk * dk,
-              "bytes_issued_per_pair_kernel": 8.0 * pairs * dk,
-              "hbm_frac_of_min_bytes": 4.0 * Kk * dk / t / HBM})
+              "flops": 3.0 * pairs * dk, "tflops": 3.0 * pairs * dk / t / 1e12,
+              "bytes_min": 4.0 * Kk * dk, "hbm_frac_of_min_bytes": 4.0 * Kk * dk / t / HBM})
         del X, Xk
+        # the C3 client count (K = 1000) on a 1M-2M column slice
+        K, d = 1000, 2_000_000
+        X = torch.empty(K, d, device="cuda")
+        fill(ctx, X, 200, 98)
+        for name, fn in (("median", bz.median), ("trimmed_mean", bz.trimmed_mean)):
+            t = timed(lambda: fn(X, {}))
+            emit({"row": "f3", "what": name, "K": K, "d": d, "ms": t * 1e3,
+                  "bytes": 4.0 * K * d, "hbm_frac": 4.0 * K * d / t / HBM})
+        Xk = X[:, :1_000_000].contiguous()
+        del X
+        t = timed(lambda: bz.Krum(Xk, {"honestSize": 800}), reps=2, warm=1)
+        pairs = K * (K + 1) / 2
+        emit({"row": "f3", "what": "Krum", "K": K, "d": Xk.shape[1], "ms": t * 1e3,
+              "flops": 3.0 * pairs * Xk.shape[1], "tflops": 3.0 * pairs * Xk.shape[1] / t / 1e12})
+        del Xk
 
     if want("c2"):
         K, d = 50, 7850
