@@ -44,9 +44,16 @@ __global__ void __launch_bounds__(256) oma_apply(float* __restrict__ X, int64_t 
 // groups of 4 columns (one float4 read + write when aligned).
 // wshift > 0: X is in the panel layout [ceil(d/W)][K][W], W = 1 << wshift, ldx = the
 // panel stride (elements); the draws are keyed the same way, so panels and rows agree.
+// ALIGNED: col_off % 4 == 0 (every unsharded call and the 256-aligned shards), so
+// a group of 4 columns is exactly one Philox block; otherwise (the shift is the same
+// for every group of the launch) a group spans two blocks.
+template <bool ALIGNED, bool VEC4>
 __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t K, int64_t d,
                                                   int64_t ldx, int64_t col_off, float sd,
-                                                  uint64_t seed, int vec4, int wshift) {
+                                                  uint64_t seed, int wshift) {
+  // x + scale*z rounds the same (no FMA) on the float4 and the scalar path, in
+  // every instantiation: a shard or a layout must reproduce the others bit for bit
+#pragma clang fp contract(off)
   typedef float f4 __attribute__((ext_vector_type(4)));
   constexpr int U = 4;                        // groups per thread per step: 4 loads in flight
   const int64_t G = (d + 3) / 4;
@@ -57,33 +64,51 @@ __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t
     const float a = h[0] * 0.70710678118654752f, b = h[1] * 0.70710678118654752f;
     const float scale = sd / sqrtf(a * a + b * b);
     float* row = wshift ? X + (k << wshift) : X + k * ldx;
-    for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g0 < G; g0 += U * T) {
-      // the loads go out before the Philox math so their latency hides behind it
-      f4 v[U];
-      float* rp[U];
-      bool full[U];
+    // Step s covers groups g0 + q*T (q < U).  Step s+1's loads are issued before
+    // step s's Philox math and stores, so each thread keeps U loads in flight
+    // across its whole loop (the draws do not depend on the data).
+    auto load = [&](int64_t g0, f4* v, float** rp, bool* full) {
 #pragma unroll
       for (int q = 0; q < U; ++q) {
         const int64_t j0 = 4 * (g0 + q * T);
         // element j of this row: row[j] (rows), or panel j >> wshift, slot j & (W-1)
         // (panels; W % 4 == 0, so a group of 4 never straddles panels)
         rp[q] = wshift ? row + (j0 >> wshift) * ldx + (j0 & ((1 << wshift) - 1)) - j0 : row;
-        full[q] = vec4 && j0 + 4 <= d;
-        v[q] = f4{0.f, 0.f, 0.f, 0.f};
-        if (full[q]) v[q] = __builtin_nontemporal_load(reinterpret_cast<f4*>(rp[q] + j0));
+        full[q] = VEC4 && j0 + 4 <= d;
+        // branch-free: a partial group loads the (aligned, valid) row start instead
+        // and takes the scalar path below.  A conditional load would merge into
+        // v[q] through a copy that waits for the load (vmcnt(0)), serialising them.
+        if constexpr (VEC4)
+          v[q] = __builtin_nontemporal_load(reinterpret_cast<f4*>(full[q] ? rp[q] + j0 : row));
       }
+    };
+    f4 v[U];
+    float* rp[U];
+    bool full[U];
+    int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g0 < G) load(g0, v, rp, full);
+    for (; g0 < G; g0 += U * T) {
+      f4 nv[U];
+      float* nrp[U];
+      bool nfull[U] = {};
+      if (g0 + U * T < G) load(g0 + U * T, nv, nrp, nfull);
 #pragma unroll
       for (int q = 0; q < U; ++q) {
         const int64_t j0 = 4 * (g0 + q * T);
         if (j0 >= d) break;
         const uint64_t c0 = (uint64_t)(col_off + j0);
-        const int sh = (int)(c0 & 3);               // unaligned shard offsets span 2 blocks
         float z[8];
         normal4_hw(seed, kStreamOmaNoise, (uint64_t)k, c0 >> 2, z);
-        if (sh) normal4_hw(seed, kStreamOmaNoise, (uint64_t)k, (c0 >> 2) + 1, z + 4);
         float add[4];
+        if constexpr (ALIGNED) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) add[u] = scale * z[u + sh];
+          for (int u = 0; u < 4; ++u) add[u] = scale * z[u];
+        } else {
+          const int sh = (int)(c0 & 3);
+          normal4_hw(seed, kStreamOmaNoise, (uint64_t)k, (c0 >> 2) + 1, z + 4);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) add[u] = scale * z[u + sh];
+        }
         if (full[q]) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) v[q][u] = v[q][u] + add[u];
@@ -93,6 +118,12 @@ __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t
           for (int u = 0; u < 4; ++u)
             if (j0 + u < d) rp[q][j0 + u] = rp[q][j0 + u] + add[u];
         }
+      }
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        v[q] = nv[q];
+        rp[q] = nrp[q];
+        full[q] = nfull[q];
       }
     }
   }
@@ -162,8 +193,19 @@ hipError_t launch_oma_philox(float* X, int64_t K, int64_t d, int64_t ldx, int64_
   const int64_t cap = std::max<int64_t>(1, (8192 + gy - 1) / gy);   // ~8K blocks in flight
   if (gx > cap) gx = cap;
   const int vec4 = (reinterpret_cast<uintptr_t>(X) % 16 == 0) && ldx % 4 == 0;
-  hipLaunchKernelGGL(oma_philox, dim3((unsigned)gx, gy), dim3(256), 0, s, X, K, d, ldx, col_off,
-                     sd, seed, vec4, wshift);
+  const dim3 grid((unsigned)gx, gy);
+  if (col_off % 4 == 0 && vec4)
+    hipLaunchKernelGGL((oma_philox<true, true>), grid, dim3(256), 0, s, X, K, d, ldx, col_off, sd,
+                       seed, wshift);
+  else if (col_off % 4 == 0)
+    hipLaunchKernelGGL((oma_philox<true, false>), grid, dim3(256), 0, s, X, K, d, ldx, col_off, sd,
+                       seed, wshift);
+  else if (vec4)
+    hipLaunchKernelGGL((oma_philox<false, true>), grid, dim3(256), 0, s, X, K, d, ldx, col_off, sd,
+                       seed, wshift);
+  else
+    hipLaunchKernelGGL((oma_philox<false, false>), grid, dim3(256), 0, s, X, K, d, ldx, col_off, sd,
+                       seed, wshift);
   return hipGetLastError();
 }
 

@@ -1,0 +1,71 @@
+"""numpy restatement of the build's counter-based noise (byzantine_aircomp_amd/csrc/philox.h).
+
+TEST INFRASTRUCTURE ONLY (see ``oracle/__init__.py``): the checker for the HIP
+Philox paths, never called by ``byzantine_aircomp_amd``.
+
+The reference draws its AirComp noise from torch's CPU generator (OMA M:385-394,
+OMA2 M:401-411); the build's production path replaces those draws with
+Philox4x32-10 (Salmon et al., SC'11) keyed by (seed, stream, iteration, index),
+so any d-shard regenerates its own columns.  This module states that keying and
+the Box-Muller transform in float64, so a GPU result can be checked draw by draw
+(the device uses the hardware log2/sqrt/sin/cos: ~1 ulp of fp32 apart).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+STREAM_OMA_CHANNEL = 0x4F4D4143
+STREAM_OMA_NOISE = 0x4F4D414E
+M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+W0, W1 = 0x9E3779B9, 0xBB67AE85
+MASK = np.uint64(0xFFFFFFFF)
+
+
+def philox4x32_10(c0, c1, c2, c3, seed: int):
+    """Philox4x32-10 on uint64 arrays holding 32-bit words (philox.h:30-41)."""
+    c = [np.asarray(x, dtype=np.uint64) & MASK for x in (c0, c1, c2, c3)]
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    for _ in range(10):
+        p0 = M0 * c[0]
+        p1 = M1 * c[2]
+        hi0, lo0 = p0 >> np.uint64(32), p0 & MASK
+        hi1, lo1 = p1 >> np.uint64(32), p1 & MASK
+        c = [hi1 ^ c[1] ^ np.uint64(k0), lo1, hi0 ^ c[3] ^ np.uint64(k1), lo0]
+        k0 = (k0 + W0) & 0xFFFFFFFF
+        k1 = (k1 + W1) & 0xFFFFFFFF
+    return c
+
+
+def _u01(v):
+    return ((v >> np.uint64(8)).astype(np.float64) + 1.0) / 16777216.0
+
+
+def normal4(seed: int, stream: int, it, idx):
+    """Four standard normals per (iteration, index) counter (philox.h normal4 / normal4_hw)."""
+    it = np.asarray(it, dtype=np.uint64)
+    idx = np.asarray(idx, dtype=np.uint64)
+    r = philox4x32_10(idx & MASK, idx >> np.uint64(32), it & MASK,
+                      np.uint64(stream) ^ (it >> np.uint64(32)), seed)
+    out = []
+    for a, b in ((r[0], r[1]), (r[2], r[3])):
+        rad = np.sqrt(-2.0 * np.log(_u01(a)))
+        t = 2.0 * np.pi * _u01(b)
+        out += [rad * np.cos(t), rad * np.sin(t)]
+    return np.stack(out, axis=-1)                   # [..., 4]
+
+
+def oma_philox(X: np.ndarray, noise_var: float, seed: int, col_off: int = 0) -> np.ndarray:
+    """X + the build's OMA noise (oma.hip oma_philox): client k's channel h_k is
+    normals 0, 1 of block (iteration 0, index k) scaled by 1/sqrt(2); element
+    (k, global column c) adds sqrt(var)/|h_k| times normal c & 3 of block
+    (iteration k, index c >> 2)."""
+    K, d = X.shape
+    h = normal4(seed, STREAM_OMA_CHANNEL, np.zeros(K, dtype=np.uint64), np.arange(K))
+    a, b = h[:, 0] / np.sqrt(2.0), h[:, 1] / np.sqrt(2.0)
+    scale = np.sqrt(noise_var) / np.sqrt(a * a + b * b)
+    cols = col_off + np.arange(d, dtype=np.uint64)
+    z = normal4(seed, STREAM_OMA_NOISE, np.arange(K, dtype=np.uint64)[:, None],
+                (cols >> np.uint64(2))[None, :])      # [K, d, 4]
+    pick = np.take_along_axis(z, (cols & np.uint64(3)).astype(np.int64)[None, :, None]
+                              .repeat(K, axis=0), axis=2)[..., 0]
+    return X.astype(np.float64) + scale[:, None] * pick

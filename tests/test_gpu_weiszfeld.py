@@ -114,6 +114,40 @@ def test_oma_philox_statistics():
     assert abs(corr) < 1e-2
 
 
+@pytest.mark.parametrize("case", ["aligned", "odd_shard", "unaligned_rows", "tail"])
+def test_oma_philox_matches_restatement(case):
+    """Every code path of the OMA Philox kernel (float4 / scalar rows, aligned or
+    odd shard offset, ragged tail) adds exactly the draws oracle/philox.py states:
+    Philox4x32-10 keyed (row, column >> 2), Box-Muller in float64 there, the
+    hardware log2/sqrt/sin/cos here (~1 ulp)."""
+    from byzantine_aircomp_amd import _lib
+    from byzantine_aircomp_amd.aggregators import Context
+    from oracle.philox import oma_philox
+    K, d, var, seed = 6, 4099, 1e-2, 91
+    ldx, off = d, 0
+    if case == "odd_shard":
+        off = 2
+    elif case == "unaligned_rows":
+        ldx = d + 1
+    elif case == "tail":
+        d = ldx = 4097
+    buf = torch.randn(K * ldx + 1, generator=torch.Generator().manual_seed(4)).cuda()
+    Xv = buf[1:] if case == "unaligned_rows" else buf[:K * ldx]     # 4-byte misaligned
+    X0 = Xv.view(K, ldx)[:, :d].cpu().numpy().copy()
+    ctx = Context(buf.device.index)
+    if off:
+        ctx.set_shard(d + off + 5, off)
+    _lib.check(ctx.lib.gm_oma_philox_f32(ctx.handle, Xv.data_ptr(), K, d, ldx, var, seed, None),
+               "gm_oma_philox_f32")
+    torch.cuda.synchronize()
+    ctx.close()
+    got = Xv.view(K, ldx)[:, :d].cpu().numpy().astype(np.float64)
+    want = oma_philox(X0, var, seed, col_off=off)
+    err = np.abs(got - want) / (1.0 + np.abs(want))
+    assert err.max() <= 2e-6, err.max()
+    assert not np.array_equal(got, X0)
+
+
 def test_gm_philox_reproducible_and_close_to_ideal():
     meta, arr = golden_case("gm_var1e-2_it5")
     X = torch.from_numpy(arr["X"]).cuda()
