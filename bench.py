@@ -69,6 +69,11 @@ def parse():
     p.add_argument("--dist", action="store_true",
                    help="take the multi-rank path (process group, RCCL comm, d-shard) even at "
                         "world size 1: a one-GPU rehearsal of the N>1 code")
+    p.add_argument("--rehearse-shard", type=int, default=0, metavar="P",
+                   help="with --dist at world size 1: run rank 0's d-shard of a P-GPU job "
+                        "(its columns, its per-iteration exchange over a 1-rank communicator): "
+                        "the per-rank time of the N=P run minus the cross-GPU all-reduce latency. "
+                        "Convergence uses the shard's sums only, so iters may differ from N=P.")
     return p.parse_args()
 
 
@@ -136,7 +141,9 @@ def main():
     from byzantine_aircomp_amd import _lib
 
     K, d_total, B = WORKLOADS[args.workload]
-    lo, hi = shard_range(d_total, world, rank)
+    if args.rehearse_shard and (world != 1 or not args.dist):
+        raise SystemExit("--rehearse-shard needs --dist at world size 1")
+    lo, hi = shard_range(d_total, args.rehearse_shard or world, rank)
     d = hi - lo
     ctx = bz.context(dev)
     if dist_path:
@@ -275,7 +282,10 @@ def main():
                                    f"Byzantine, tol 1e-5, maxiter {args.maxiter}"
                                    + (f", noise_var {args.var}" if args.agg == "gm" else ""),
                        "K": K, "d": d_total, "byzantine": B, "iters": res.iters,
-                       "algo": res.algo, "layout": layout, "parallelism": f"d-shard x{world}" if dist_path else "none",
+                       "algo": res.algo, "layout": layout,
+                       "parallelism": (f"rehearsal: rank 0 of a d-shard x{args.rehearse_shard} "
+                                       f"job on 1 GPU (d_local {d})" if args.rehearse_shard else
+                                       f"d-shard x{world}" if dist_path else "none"),
                        "passes_per_aggregation": 2 if res.algo.startswith("gram") else res.iters + 1},
             "roofline": roof,
             "cpu_baseline": None,
