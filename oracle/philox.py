@@ -69,3 +69,42 @@ def oma_philox(X: np.ndarray, noise_var: float, seed: int, col_off: int = 0) -> 
     pick = np.take_along_axis(z, (cols & np.uint64(3)).astype(np.int64)[None, :, None]
                               .repeat(K, axis=0), axis=2)[..., 0]
     return X.astype(np.float64) + scale[:, None] * pick
+
+
+STREAM_CHANNEL = 0x43484E4C
+STREAM_NOISE = 0x4E4F4953
+
+
+def gm_draws(seed: int, d_total: int, col_off: int = 0):
+    """A ``draw(shape, std)`` for ``oracle.aggregators.gm`` that supplies the build's
+    Philox AirComp draws in the reference's per-iteration order (OMA2 M:401-402,
+    M:411: channel real [K], channel imag [K], noise [d+1]).  Iteration it's client
+    k takes normals 0 / 1 of block (it, k) on the channel stream (weiszfeld.hip
+    kspace_step); column j's noise is normal 0 of block (it, global j) on the noise
+    stream, the denominator's entry is global index d_total (stream_pass.hip)."""
+    import torch
+    state = {"it": 0, "call": 0, "h": None}
+
+    def draw(shape, std):
+        it, call = state["it"], state["call"]
+        if call == 0:
+            n = shape[0]
+            state["h"] = normal4(seed, STREAM_CHANNEL, np.uint64(it), np.arange(n, dtype=np.uint64))
+            v = state["h"][:, 0]
+        elif call == 1:
+            v = state["h"][:, 1]
+        else:
+            L = shape[0]                                  # d + 1
+            idx = np.concatenate([col_off + np.arange(L - 1, dtype=np.uint64),
+                                  np.array([d_total], dtype=np.uint64)])
+            v = normal4(seed, STREAM_NOISE, np.uint64(it), idx)[:, 0]
+        state["call"] = call + 1
+        if call == 2 or (call == 1 and state.get("no_noise")):
+            state["it"], state["call"] = it + 1, 0
+        return torch.from_numpy((v * std).astype(np.float32))
+
+    def no_noise():
+        state["no_noise"] = True
+
+    draw.no_noise = no_noise
+    return draw

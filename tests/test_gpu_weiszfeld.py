@@ -148,6 +148,31 @@ def test_oma_philox_matches_restatement(case):
     assert not np.array_equal(got, X0)
 
 
+@pytest.mark.parametrize("maxiter,var", [(3, 1e-2), (40, 1e-3), (25, None)])
+def test_gm_philox_matches_restatement(maxiter, var):
+    """The production AirComp path (Philox draws on the device) against the oracle gm
+    (M:131-160, op for op) fed the same draws from oracle/philox.py: channel per
+    (iteration, client), noise per (iteration, global column), denominator noise at
+    index d.  Tolerance: relative L2 1e-5 (north_star), identical iteration count."""
+    from oracle.philox import gm_draws
+    meta, arr = golden_case("gm_var1e-2_it5")
+    X = torch.from_numpy(arr["X"].copy())
+    o = {"maxiter": maxiter, "tol": 1e-5, "noise_var": var, "P_max": 1}
+    if meta.get("guess_supplied"):
+        o["guess"] = torch.from_numpy(arr["guess"].copy())
+    gpu_o = dict(o, seed=4242)
+    if "guess" in o:
+        gpu_o["guess"] = o["guess"].cuda()
+    got = bz().gm(X.cuda(), gpu_o)
+    it = bz().aggregators.last_result.iters
+    draw = gm_draws(4242, X.shape[1])
+    if var is None:
+        draw.no_noise()
+    ref, tr = orc.gm(X, o, draw=draw)
+    assert it == tr.iters
+    assert rel_l2(got.cpu().numpy(), ref.numpy()) <= 1e-5
+
+
 def test_gm_philox_reproducible_and_close_to_ideal():
     meta, arr = golden_case("gm_var1e-2_it5")
     X = torch.from_numpy(arr["X"]).cuda()
