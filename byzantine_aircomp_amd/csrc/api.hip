@@ -666,6 +666,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   int64_t pending = -1;   // iteration whose KState copy is in flight (lagged)
 
   int64_t t = 0, enqueued = 0;
+  const KState* final_st = nullptr;   // set when a lagged poll already saw the stop
   for (; t < o->maxiter; ++t) {
     rc = do_pass(t);
     if (rc) return rc;
@@ -695,7 +696,10 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       HIPCHK(hipEventRecord(c->poll_ev[t & 1], s));
       if (pending >= 0) {
         HIPCHK(hipEventSynchronize(c->poll_ev[pending & 1]));
-        if (hslot[pending & 1].done) break;
+        if (hslot[pending & 1].done) {
+          final_st = &hslot[pending & 1];
+          break;
+        }
       }
       pending = t;
       continue;
@@ -706,11 +710,17 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       if (hst->done) break;
     }
   }
-  rc = poll(hst);
-  if (rc) return rc;
-  r.iters = hst->iters;
-  r.last_movement = hst->last_movement;
-  r.converged = hst->converged;
+  // The state the lagged poll saw is final (launches after the stop are no-ops and
+  // leave it alone), so no second copy + sync: the host returns while the device
+  // drains the queued no-op iteration, and the next call's work queues behind it.
+  if (!final_st) {
+    rc = poll(hst);
+    if (rc) return rc;
+    final_st = hst;
+  }
+  r.iters = final_st->iters;
+  r.last_movement = final_st->last_movement;
+  r.converged = final_st->converged;
   r.algo_used = algo;
   if (r.iters < 1) return fail(GM_ERR_HIP, "Weiszfeld loop recorded no iteration");
   // passes queued after the stop (lagged poll) exited at once: not timed as passes
