@@ -361,7 +361,9 @@ static const void* pass_fn(bool panel) {
   if (pass_variant() == 1)
     return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 1, OCC>);
 #endif
-  if (pass_variant() == 2)
+  // Row-major STEP passes with float4 rows also take the rolling prefetch: C5's
+  // batched K=50 tile streams 4.64 vs 4.43 TB/s (profiles/r04_c5_roll_ab.txt).
+  if (pass_variant() == 2 || (pass_variant() < 0 && MODE == 0 && V == 4))
     return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 2, OCC>);
   return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 0, OCC>);
 }
