@@ -188,17 +188,20 @@ __global__ void __launch_bounds__(256) col_select(const float* __restrict__ X, i
 
 // Krum, step 1: squared distances of every row pair, register-tiled.
 // A block owns a 128 x 128 tile of pairs (row tiles bi <= bj: D is symmetric)
-// over one slice of the columns; each thread an 8 x 8 sub-tile.  Per 32-column
-// stage both row tiles go to LDS column-major (sA[c][r]), so a thread reads its
-// 8 rows of one column as two ds_read_b128 and does 64 (sub, fma) pairs: the
+// over one slice of the columns; each of 512 threads an 8 x 4 sub-tile (8 x 8 with
+// 256 threads needed 326 VGPRs: one wave per SIMD, the LDS reads exposed).  Per
+// 32-column stage both row tiles go to LDS column-major (sA[c][r]), so a thread
+// reads its 8 + 4 values of one column as three ds_read_b128 and does 32 (sub, fma)
+// pairs (packed two at a time by the compiler): the
 // exact differences of M:199 in fp32, squares summed in fp32 over the stage and
 // in fp64 across stages.  Slices write fp64 partials [S][K][K]; pair_reduce sums
 // them in a fixed order (deterministic, no atomics).
 constexpr int kPT = 128;   // pair-tile edge (rows)
 constexpr int kPC = 32;    // columns per LDS stage
+constexpr int kPDT = 512;  // pair_dist threads per block
 
 template <bool VEC>
-__global__ void __launch_bounds__(256) pair_dist(const float* __restrict__ X, int64_t K,
+__global__ void __launch_bounds__(kPDT) pair_dist(const float* __restrict__ X, int64_t K,
                                                  int64_t d, int64_t ldx, int64_t chunk,
                                                  double* __restrict__ part) {
   typedef float f4 __attribute__((ext_vector_type(4)));
@@ -209,19 +212,19 @@ __global__ void __launch_bounds__(256) pair_dist(const float* __restrict__ X, in
   while (p >= nT - bi) { p -= nT - bi; ++bi; }
   const int64_t bj = bi + p;
   const int64_t cb = (int64_t)blockIdx.y * chunk, ce = cb + chunk < d ? cb + chunk : d;
-  const int ti = threadIdx.x >> 4, tj = threadIdx.x & 15;
-  double accd[8][8];
+  const int ti = threadIdx.x >> 5, tj = threadIdx.x & 31;
+  double accd[8][4];
 #pragma unroll
   for (int u = 0; u < 8; ++u)
 #pragma unroll
-    for (int v = 0; v < 8; ++v) accd[u][v] = 0.0;
-  // stage loads: thread owns (row r, columns cg..cg+3) of both row tiles for q = 0..3;
+    for (int v = 0; v < 4; ++v) accd[u][v] = 0.0;
+  // stage loads: thread owns (row r, columns cg..cg+3) of both row tiles for q = 0..1;
   // the next stage's loads are issued before this stage's arithmetic (register prefetch)
-  f4 pre[4][2];
+  f4 pre[2][2];
   auto load_stage = [&](int64_t c0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int idx = threadIdx.x + 256 * q, r = idx >> 3, cg = (idx & 7) * 4;
+    for (int q = 0; q < 2; ++q) {
+      const int idx = threadIdx.x + kPDT * q, r = idx >> 3, cg = (idx & 7) * 4;
       const int64_t col = c0 + cg;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -244,8 +247,8 @@ __global__ void __launch_bounds__(256) pair_dist(const float* __restrict__ X, in
   for (int64_t c0 = cb; c0 < ce; c0 += kPC) {
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int idx = threadIdx.x + 256 * q, r = idx >> 3, cg = (idx & 7) * 4;
+    for (int q = 0; q < 2; ++q) {
+      const int idx = threadIdx.x + kPDT * q, r = idx >> 3, cg = (idx & 7) * 4;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         sA[cg + u][r] = pre[q][0][u];
@@ -254,23 +257,22 @@ __global__ void __launch_bounds__(256) pair_dist(const float* __restrict__ X, in
     }
     __syncthreads();
     if (c0 + kPC < ce) load_stage(c0 + kPC);
-    float acc[8][8];
+    float acc[8][4];
 #pragma unroll
     for (int u = 0; u < 8; ++u)
 #pragma unroll
-      for (int v = 0; v < 8; ++v) acc[u][v] = 0.f;
+      for (int v = 0; v < 4; ++v) acc[u][v] = 0.f;
 #pragma unroll 4
     for (int c = 0; c < kPC; ++c) {
       const f4 a0 = *reinterpret_cast<const f4*>(&sA[c][ti * 8]);
       const f4 a1 = *reinterpret_cast<const f4*>(&sA[c][ti * 8 + 4]);
-      const f4 b0 = *reinterpret_cast<const f4*>(&sB[c][tj * 8]);
-      const f4 b1 = *reinterpret_cast<const f4*>(&sB[c][tj * 8 + 4]);
+      const f4 b0 = *reinterpret_cast<const f4*>(&sB[c][tj * 4]);
       const float a[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-      const float b[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+      const float b[4] = {b0[0], b0[1], b0[2], b0[3]};
 #pragma unroll
       for (int u = 0; u < 8; ++u)
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
+        for (int v = 0; v < 4; ++v) {
           const float t = a[u] - b[v];
           acc[u][v] = fmaf(t, t, acc[u][v]);
         }
@@ -278,7 +280,7 @@ __global__ void __launch_bounds__(256) pair_dist(const float* __restrict__ X, in
 #pragma unroll
     for (int u = 0; u < 8; ++u)
 #pragma unroll
-      for (int v = 0; v < 8; ++v) accd[u][v] += (double)acc[u][v];
+      for (int v = 0; v < 4; ++v) accd[u][v] += (double)acc[u][v];
   }
   double* P = part + (int64_t)blockIdx.y * K * K;
 #pragma unroll
@@ -286,8 +288,8 @@ __global__ void __launch_bounds__(256) pair_dist(const float* __restrict__ X, in
     const int64_t i = bi * kPT + ti * 8 + u;
     if (i >= K) break;
 #pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      const int64_t j = bj * kPT + tj * 8 + v;
+    for (int v = 0; v < 4; ++v) {
+      const int64_t j = bj * kPT + tj * 4 + v;
       if (j < K) P[i * K + j] = accd[u][v];
     }
   }
@@ -398,7 +400,7 @@ int64_t krum_slices(int64_t K, int64_t d) {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pair_dist<true>, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pair_dist<true>, kPDT, 0) != hipSuccess ||
         occ < 1)
       occ = 1;
     per_round = cus * occ;
@@ -425,10 +427,10 @@ hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_
   const int64_t chunk = ((d + S - 1) / S + kPC - 1) / kPC * kPC;
   const bool vec = reinterpret_cast<uintptr_t>(X) % 16 == 0 && ldx % 4 == 0;
   if (vec)
-    hipLaunchKernelGGL(pair_dist<true>, dim3((unsigned)pairs, (unsigned)S), dim3(256), 0, s, X, K,
+    hipLaunchKernelGGL(pair_dist<true>, dim3((unsigned)pairs, (unsigned)S), dim3(kPDT), 0, s, X, K,
                        d, ldx, chunk, part);
   else
-    hipLaunchKernelGGL(pair_dist<false>, dim3((unsigned)pairs, (unsigned)S), dim3(256), 0, s, X,
+    hipLaunchKernelGGL(pair_dist<false>, dim3((unsigned)pairs, (unsigned)S), dim3(kPDT), 0, s, X,
                        K, d, ldx, chunk, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
