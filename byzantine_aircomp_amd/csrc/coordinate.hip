@@ -62,14 +62,18 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int q = 0; q < NR; ++q) ans[c][q] = 0;
+  // counts fit 32 bits (K <= 2048): one scalar add per ballot instead of a 64-bit pair
+  int rr[NR];
+#pragma unroll
+  for (int q = 0; q < NR; ++q) rr[q] = (int)r[q];
   for (int bit = 31; bit >= 0; --bit) {
-    int64_t cnt[NC][NR];
+    int cnt[NC][NR];
 #pragma unroll
     for (int c = 0; c < NC; ++c)
 #pragma unroll
       for (int q = 0; q < NR; ++q) {
         const uint32_t t = ans[c][q] | (1u << bit);
-        int64_t n = 0;
+        int n = 0;
 #pragma unroll
         for (int i = 0; i < R; ++i) n += __popcll(__ballot(key[c][i] < t));
         cnt[c][q] = n;
@@ -78,7 +82,7 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
     for (int c = 0; c < NC; ++c)
 #pragma unroll
       for (int q = 0; q < NR; ++q)
-        if (cnt[c][q] <= r[q]) ans[c][q] |= 1u << bit;
+        if (cnt[c][q] <= rr[q]) ans[c][q] |= 1u << bit;
   }
 }
 
