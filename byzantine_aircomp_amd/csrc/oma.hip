@@ -55,7 +55,10 @@ __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t
   // every instantiation: a shard or a layout must reproduce the others bit for bit
 #pragma clang fp contract(off)
   typedef float f4 __attribute__((ext_vector_type(4)));
-  constexpr int U = 4;                        // groups per thread per step: 4 loads in flight
+#ifndef GMK_OMA_U
+#define GMK_OMA_U 4
+#endif
+  constexpr int U = GMK_OMA_U;                // groups per thread per step: U=4 17.4 ms vs U=2 17.7 at C3 size
   const int64_t G = (d + 3) / 4;
   const int64_t T = (int64_t)gridDim.x * blockDim.x;
   for (int64_t k = blockIdx.y; k < K; k += gridDim.y) {
