@@ -18,6 +18,10 @@
 #include "gmagg_internal.h"
 #include "philox.h"
 
+#ifndef GMK_RES_SLEEP
+#define GMK_RES_SLEEP 1   // spin back-off of the grid barrier (A/B knob)
+#endif
+
 namespace gmk {
 
 // (ResArgs: gmagg_internal.h)
@@ -40,7 +44,9 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned nblocks, unsig
     } else {
       unsigned spins = 0;
       while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
-        __builtin_amdgcn_s_sleep(1);
+#if GMK_RES_SLEEP > 0
+        __builtin_amdgcn_s_sleep(GMK_RES_SLEEP);
+#endif
         if (++spins > (1u << 24) ||
             __hip_atomic_load(&bar[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
           __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
