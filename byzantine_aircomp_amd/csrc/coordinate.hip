@@ -13,14 +13,39 @@
 
 namespace gmk {
 
-// mean: one thread per column, fp64 accumulation.
+// mean: W consecutive columns per thread (W = 4: one float4 per row, 1 KiB per wave
+// instruction), 8 rows' loads in flight, each column summed in fp64 in row order
+// and rounded once (the same sums for every W).
+template <int W>
 __global__ void __launch_bounds__(256) col_mean(const float* __restrict__ X, int64_t K, int64_t d,
                                                 int64_t ldx, float* __restrict__ out) {
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d;
-       j += (int64_t)gridDim.x * blockDim.x) {
-    double s = 0.0;
-    for (int64_t k = 0; k < K; ++k) s += (double)X[k * ldx + j];
-    out[j] = (float)(s / (double)K);
+  typedef float fv __attribute__((ext_vector_type(W)));
+  constexpr int U = 8;
+  const int64_t G = d / W;            // W > 1: d % W == 0 (checked by the launcher)
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const float* col = X + g * W;
+    double s[W];
+#pragma unroll
+    for (int v = 0; v < W; ++v) s[v] = 0.0;
+    int64_t k = 0;
+    for (; k + U <= K; k += U) {
+      fv x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        x[u] = __builtin_nontemporal_load(reinterpret_cast<const fv*>(col + (k + u) * ldx));
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int v = 0; v < W; ++v) s[v] += (double)x[u][v];
+    }
+    for (; k < K; ++k) {
+      const fv x = *reinterpret_cast<const fv*>(col + k * ldx);
+#pragma unroll
+      for (int v = 0; v < W; ++v) s[v] += (double)x[v];
+    }
+#pragma unroll
+    for (int v = 0; v < W; ++v) out[g * W + v] = (float)(s[v] / (double)K);
   }
 }
 
@@ -374,7 +399,11 @@ static int grid_cols(int64_t d) {
 
 hipError_t launch_col_mean(const float* X, int64_t K, int64_t d, int64_t ldx, float* out,
                            hipStream_t s) {
-  hipLaunchKernelGGL(col_mean, dim3(grid_cols(d)), dim3(256), 0, s, X, K, d, ldx, out);
+  const bool vec4 = reinterpret_cast<uintptr_t>(X) % 16 == 0 && ldx % 4 == 0 && d % 4 == 0;
+  if (vec4)
+    hipLaunchKernelGGL(col_mean<4>, dim3(grid_cols(d / 4)), dim3(256), 0, s, X, K, d, ldx, out);
+  else
+    hipLaunchKernelGGL(col_mean<1>, dim3(grid_cols(d)), dim3(256), 0, s, X, K, d, ldx, out);
   return hipGetLastError();
 }
 
