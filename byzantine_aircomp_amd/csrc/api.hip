@@ -949,6 +949,17 @@ int gm_oma_philox_panels_f32(gm_ctx* c, float* X, int64_t K, int64_t d, int64_t 
   return GM_OK;
 }
 
+int gm_rows_to_panels_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
+                          float* P, int64_t W, int64_t panel_stride, void* stream) {
+  if (!c || !X || !P || K < 0 || d < 0 || ldx < d || W < 1 || panel_stride < K * W)
+    return fail(GM_ERR_INVALID, "gm_rows_to_panels_f32: bad args");
+  if (K == 0 || d == 0) return GM_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(launch_rows_to_panels(X, K, d, ldx, P, W, panel_stride,
+                               reinterpret_cast<hipStream_t>(stream)));
+  return GM_OK;
+}
+
 int gm_oma_apply_f32(gm_ctx* c, float* X, int64_t K, int64_t d, int64_t ldx, const float* hr,
                      const float* hi, const float* nr, const float* ni, void* stream) {
   if (!c || !X || !hr || !hi || !nr || !ni || K < 0 || d < 0 || ldx < d)

@@ -142,6 +142,8 @@ hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_
 // OMA / synthetic fills (oma.hip).
 hipError_t launch_oma_apply(float* X, int64_t K, int64_t d, int64_t ldx, const float* hr,
                             const float* hi, const float* nr, const float* ni, hipStream_t s);
+hipError_t launch_rows_to_panels(const float* X, int64_t K, int64_t d, int64_t ldx, float* P,
+                                 int64_t W, int64_t pstride, hipStream_t s);
 hipError_t launch_oma_philox(float* X, int64_t K, int64_t d, int64_t ldx, int64_t d_total,
                              int64_t col_off, float sd, uint64_t seed, hipStream_t s,
                              int wshift = 0);

@@ -78,6 +78,20 @@ class ClientPanels:
         if tuple(X.shape) != (self.K, self.d):
             raise ValueError(f"rows must be [{self.K}, {self.d}] (got {tuple(X.shape)})")
         X = X.to(self.device)
+        if X.device.type == "cuda" and X.dtype == torch.float32:
+            # one HIP kernel (pack.hip, gm_rows_to_panels_f32) instead of torch's
+            # transposed copy
+            from . import _lib
+            from .aggregators import context, _stream_ptr
+            if X.stride(1) != 1 or X.stride(0) < self.d:
+                X = X.contiguous()
+            ctx = context(X.device)
+            with torch.cuda.device(X.device):
+                _lib.check(ctx.lib.gm_rows_to_panels_f32(
+                    ctx.handle, X.data_ptr(), self.K, self.d, max(X.stride(0), self.d),
+                    self.data.data_ptr(), self.W, self.panel_stride, _stream_ptr(X.device)),
+                    "gm_rows_to_panels_f32")
+            return self
         nf = self._full()
         with torch.no_grad():
             if nf:

@@ -175,6 +175,13 @@ int gm_oma_philox_f32(gm_ctx* ctx, float* X, int64_t K, int64_t d, int64_t ldx,
 int gm_oma_philox_panels_f32(gm_ctx* ctx, float* X, int64_t K, int64_t d, int64_t panel_stride,
                              double noise_var, uint64_t seed, void* stream);
 
+/* Caller-side packing (row f2): copy the row-major client matrix X[K][ldx] (the
+ * reference's flatten_list stack, MNIST_Air_weight.py:206-209) into the panel layout
+ * P = [ceil(d/W)][K][W] with panel_stride >= K*W elements between panels
+ * (GM_LAYOUT_PANELS).  Padding columns >= d are not written. */
+int gm_rows_to_panels_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t ldx,
+                          float* P, int64_t W, int64_t panel_stride, void* stream);
+
 /* OMA with the reference's own draws (device arrays): h_re[K], h_im[K],
  * n_re[K*d], n_im[K*d] (row-major, already scaled by sqrt(noise_var)).
  * Bit-exact with the reference's fp32 op order. */

@@ -110,3 +110,25 @@ def test_oma_philox_on_panels_equals_rows(K, d):
     assert torch.equal(P.to_rows(), X)
     if d % P.W:
         assert torch.count_nonzero(P.data[-1, :, d % P.W:]) == 0
+
+
+@pytest.mark.parametrize("K,d,W,offset", [(1000, 4099, None, 0), (3, 37, None, 0), (50, 7850, None, 1),
+                                          (7, 100, 6, 0), (600, 8192, None, 0)])
+def test_rows_to_panels_kernel_matches_layout(K, d, W, offset):
+    """gm_rows_to_panels_f32 (pack.hip) writes exactly the panel image of the rows:
+    float4 and scalar paths (misaligned rows, W not a multiple of 4), ragged last
+    panel with its padding left zero."""
+    from byzantine_aircomp_amd.panels import ClientPanels
+    g = torch.Generator().manual_seed(K + d)
+    buf = torch.randn(K * d + offset, generator=g).cuda()
+    X = buf[offset:].view(K, d)
+    P = ClientPanels(K, d, W=W)
+    P.copy_rows_(X)
+    torch.cuda.synchronize()
+    Wd = P.W
+    npan = -(-d // Wd)
+    ref = torch.zeros(K, npan * Wd)
+    ref[:, :d] = X.cpu()
+    ref = ref.view(K, npan, Wd).transpose(0, 1)
+    assert torch.equal(P.data.cpu(), ref)
+    assert torch.equal(P.to_rows().cpu(), X.cpu())
