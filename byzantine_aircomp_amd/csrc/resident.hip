@@ -22,6 +22,19 @@
 #define GMK_RES_SLEEP 1   // spin back-off of the grid barrier (A/B knob)
 #endif
 
+// -DGMK_RES_PROF: block 0 / thread 0 accumulates s_memrealtime (100 MHz) deltas per
+// phase of the iteration and prints them at the end (timing probe builds only).
+#ifdef GMK_RES_PROF
+#define RES_T(i)                                                        \
+  if (blockIdx.x == 0 && threadIdx.x == 0) {                            \
+    const uint64_t now_ = __builtin_amdgcn_s_memrealtime();             \
+    prof_[i] += now_ - prev_;                                           \
+    prev_ = now_;                                                       \
+  }
+#else
+#define RES_T(i)
+#endif
+
 namespace gmk {
 
 // (ResArgs: gmagg_internal.h)
@@ -173,6 +186,10 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   int64_t it = 0;
   double last_mv = NAN;
   int conv = 0;
+#ifdef GMK_RES_PROF
+  uint64_t prof_[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t prev_ = __builtin_amdgcn_s_memrealtime();
+#endif
   for (;; ++it) {
     // (1) reduce the previous pass's partials, same order in every block: the
     // slab columns needed (D2, at it = 0 also r, then mv2 / gn2) are spread over
@@ -206,6 +223,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
       }
     }
     __syncthreads();
+    RES_T(0)
     // (2) tol test of the pass that produced g_it (M:180-183)
     if (it >= 1) {
       const float mv = (float)sqrt(s_tot[0]);
@@ -250,6 +268,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
       if (tid == 0) s_anoise = a.has_noise ? (float)(scale * a.noise_sd) : 0.f;
     }
     __syncthreads();
+    RES_T(1)
 
     // (4) phase A on the resident tile
     float wt[R];
@@ -292,6 +311,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
       s_g[tid] = gnew;
     }
     __syncthreads();
+    RES_T(2)
     // (5) phase B: distances to the new iterate
     float gv[V];
 #pragma unroll
@@ -311,9 +331,18 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
     double racc[RPL];
 #pragma unroll
     for (int m = 0; m < RPL; ++m) racc[m] = e[m];
+    RES_T(3)
     publish((int)((it + 1) & 1), racc, nullptr, mvp, gnp);
+    RES_T(4)
     if (!grid_sync(a.bar, nb, gen, &s_ok)) return;
+    RES_T(5)
   }
+#ifdef GMK_RES_PROF
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    printf("GMK_RES_PROF nb=%u iters=%ld ns/iter: reduce %.0f coef %.0f phaseA %.0f phaseB %.0f "
+           "publish %.0f barrier %.0f\n", nb, (long)it, 10.0 * prof_[0] / it, 10.0 * prof_[1] / it,
+           10.0 * prof_[2] / it, 10.0 * prof_[3] / it, 10.0 * prof_[4] / it, 10.0 * prof_[5] / it);
+#endif
 
   if (fin) a.out[gj] = gcur;
   if (blockIdx.x == 0 && tid == 0) {
