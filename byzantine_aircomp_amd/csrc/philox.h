@@ -89,13 +89,19 @@ __device__ __forceinline__ void normal4_hw(uint64_t seed, uint32_t stream, uint6
   box_muller_hw(r.z, r.w, &out[2], &out[3]);
 }
 
-// One standard normal for element `idx` (uses half of a Philox block).
+// One standard normal for element `idx` (uses half of a Philox block): the AirComp
+// column noise, drawn by the pass's finisher threads between two block barriers, so
+// the device takes the hardware Box-Muller (every device call site alike).
 __host__ __device__ __forceinline__ float normal1(uint64_t seed, uint32_t stream, uint64_t iter,
                                                   uint64_t idx) {
   u4 c{(uint32_t)idx, (uint32_t)(idx >> 32), (uint32_t)iter, stream ^ (uint32_t)(iter >> 32)};
   u4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
   float n0, n1;
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(GMK_NORMAL1_PRECISE)   // A/B knob
+  box_muller_hw(r.x, r.y, &n0, &n1);
+#else
   box_muller(r.x, r.y, &n0, &n1);
+#endif
   return n0;
 }
 
