@@ -1,29 +1,34 @@
 """Benchmark: geometric-median aggregations/sec at K=1000, d=11M (BASELINE.json).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W] [--workload c3|c4-shard|c2|...]
     torchrun --nproc-per-node N bench.py --gpus N ...     (the driver's N>1 form)
 
-One step = one full `gm2` aggregation (BASELINE config C3): the initial
-distance pass plus Weiszfeld iterations until the reference's tol test
-(||g_t - g_{t+1}|| <= 1e-5) fires, on a synthetic K=1000 x d=11M fp32 client
-matrix already resident in HBM (honest rows ~ N(0, 0.05^2), the last 20% ~
-N(0.25, 0.5^2), guess ~ N(0, 0.01^2); generated on the device by Philox).
+One step = one full aggregation: for the default workload (BASELINE config C3)
+one `gm2` call — the initial distance pass plus Weiszfeld iterations until the
+reference's tol test (||g_t - g_{t+1}|| <= 1e-5) fires — on a synthetic
+K=1000 x d=11M fp32 client matrix already resident in HBM (honest rows ~
+N(0, 0.05^2), the last 20% ~ N(0.25, 0.5^2), guess ~ N(0, 0.01^2); generated on
+the device by Philox).  `--workload c2` is BASELINE config C2 (AirComp `gm`,
+var 1e-2, K=50 x d=7850, 1000 iterations); `c4-shard` one GPU's shard of C4.
 
-N > 1: d is sharded over the ranks (256-aligned contiguous column shards),
-each Weiszfeld iteration all-reduces a (K+2)-vector of fp64 partials over RCCL
-(xGMI), every rank takes the same stop decision; total work is fixed, so
-scaling is "strong".  value = aggregations/s of the whole job.
+N > 1: d is sharded over the ranks (sharded.ShardedGM: 256-aligned contiguous
+column shards), each Weiszfeld iteration all-reduces a (K+2)-vector of fp64
+partials over RCCL (xGMI), every rank takes the same stop decision; total work
+is fixed, so scaling is "strong".  value = aggregations/s of the whole job.
 
 Rank 0 prints ONE JSON line.  `roofline` prices the dominant kernel (the fused
 streaming pass: 4*K*d_local algorithmic bytes per launch) with HIP events the
-library records around every launch on its stream; `cpu_baseline` times the
-CPU oracle (an op-for-op PyTorch-CPU restatement of the reference's gm2) on a
-bounded sample on this host.
+library records around every launch on its stream, and the whole aggregation
+(4*K*d_local*(passes) / ms_per_step); `cpu_baseline` times the CPU oracle (an
+op-for-op PyTorch-CPU restatement of the reference's gm2 / gm) on a bounded
+sample on this host; `check` is a full-size correctness check of the returned
+aggregate (the fp64 Weiszfeld fixed-point step at g, all ranks).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -34,14 +39,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "GM aggregations/sec at K=1000,d=11M; % HBM roofline; 1/2/4/8 GPUs"
 
 WORKLOADS = {
-    # name: (K, d, byzantine rows)
-    "c3": (1000, 11_000_000, 200),
-    "c3-small": (1000, 1_000_000, 200),
-    "c4-shard": (256, 15_625_000, 51),     # one GPU's shard of K=256 x d=125M
-    "c5-problem": (50, 100_000, 10),
-    "c2": (50, 7850, 10),                   # MNIST MLP d, K=50, B=10 (use --agg gm --var 1e-2)
+    # name: (K, d, byzantine rows, default aggregator, default noise variance)
+    "c3": (1000, 11_000_000, 200, "gm2", None),
+    "c3-small": (1000, 1_000_000, 200, "gm2", None),
+    "c4-shard": (256, 15_625_000, 51, "gm2", None),     # one GPU's shard of K=256 x d=125M
+    "c4": (256, 125_000_000, 51, "gm2", None),          # the whole C4 job (d-sharded over N)
+    "c5-problem": (50, 100_000, 10, "gm2", None),
+    "c2": (50, 7850, 10, "gm", 1e-2),                   # MNIST MLP d, K=50, B=10, AirComp gm
 }
 MFMA_F32_PEAK_TFLOPS = 157.3                 # v_mfma_f32_32x32x2_f32, dense (MI355X_MICROARCH.md)
 MFMA_BF16_PEAK_TFLOPS = 2516.6               # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz, dense
@@ -54,8 +61,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     p.add_argument("--algo", default="auto", choices=["auto", "stream", "twopass", "gram", "gram_f32"])
-    p.add_argument("--agg", default="gm2", choices=["gm2", "gm"])
-    p.add_argument("--var", type=float, default=None, help="gm noise variance (None = no AWGN)")
+    p.add_argument("--agg", default=None, choices=["gm2", "gm"],
+                   help="aggregator (default: the workload's — gm2, or gm for c2)")
+    p.add_argument("--var", type=float, default=None,
+                   help="gm noise variance (default: the workload's; None = no AWGN)")
     p.add_argument("--maxiter", type=int, default=1000)
     p.add_argument("--layout", default="auto", choices=["auto", "rows", "panels"],
                    help="client matrix layout: rows = the reference's [K, d] stack; panels = "
@@ -65,61 +74,119 @@ def parse():
     p.add_argument("--alt-steps", type=int, default=None,
                    help="steps for the other layout's measurement (0 = skip)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    p.add_argument("--cpu-d", type=int, default=2_000_000, help="CPU sample width")
+    p.add_argument("--cpu-d", type=int, default=2_000_000, help="CPU sample width (columns)")
+    p.add_argument("--cpu-budget", type=float, default=20.0,
+                   help="seconds of CPU work the baseline sample aims for")
+    p.add_argument("--no-check", action="store_true", help="skip the full-size correctness check")
     p.add_argument("--dist", action="store_true",
-                   help="take the multi-rank path (process group, RCCL comm, d-shard) even at "
+                   help="take the multi-rank path (process group, ShardedGM, RCCL comm) even at "
                         "world size 1: a one-GPU rehearsal of the N>1 code")
     p.add_argument("--rehearse-shard", type=int, default=0, metavar="P",
                    help="with --dist at world size 1: run rank 0's d-shard of a P-GPU job "
                         "(its columns, its per-iteration exchange over a 1-rank communicator): "
                         "the per-rank time of the N=P run minus the cross-GPU all-reduce latency. "
                         "Convergence uses the shard's sums only, so iters may differ from N=P.")
+    p.add_argument("--one-gpu", action="store_true",
+                   help="N>1 rehearsal on a one-GPU box: every rank on cuda:0, gloo process "
+                        "group, the torch all-reduce callback instead of RCCL (timing is not "
+                        "a scaling measurement)")
     return p.parse_args()
 
 
-def shard_range(d, n, r, align=256):
-    per = -(-d // n)
-    per = -(-per // align) * align
-    lo = min(d, r * per)
-    return lo, min(d, lo + per)
+def host_cpu_share() -> int:
+    """CPUs this process may use: its affinity set, capped by a cgroup CPU quota
+    (on the GPU box os.cpu_count() shows the whole machine, not this box's share)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
-def pmc_traffic(workload, layout):
-    """Per-launch HBM bytes of the STEP pass from the newest committed PMC summary
-    (rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same bench workload and
-    layout; tools/pmc_summary.py applies the gfx950 FETCH_SIZE x2 correction)."""
+def pmc_traffic(workload, layout, kernel="weiszfeld_pass", mode="0"):
+    """Per-launch HBM bytes of the dominant kernel from the newest committed PMC
+    summary (rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same bench workload
+    and layout; tools/pmc_summary.py applies the gfx950 FETCH_SIZE x2 correction)."""
     import glob
     import re
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}*.json")))
     for path in reversed(files):
         data = json.load(open(path))
         for name, row in data["kernels"].items():
-            m = re.search(r"weiszfeld_pass<([^>]*)>", name)
-            if not m:
-                continue
-            targs = m.group(1).split(", ")        # <V,NW,LPR,R,MODE,SCHED,OCC[,PANEL]>
-            panel = len(targs) == 8 and targs[7] == "true"
-            if targs[4] == "0" and panel == (layout == "panels"):
+            if kernel == "weiszfeld_pass":
+                m = re.search(r"weiszfeld_pass<([^>]*)>", name)
+                if not m:
+                    continue
+                targs = m.group(1).split(", ")        # <V,NW,LPR,R,MODE,SCHED,OCC[,PANEL]>
+                panel = len(targs) == 8 and targs[7] == "true"
+                if targs[4] == mode and panel == (layout == "panels"):
+                    return row["hbm_bytes_per_launch"] / 1e9, os.path.relpath(path, ROOT)
+            elif kernel in name:
                 return row["hbm_bytes_per_launch"] / 1e9, os.path.relpath(path, ROOT)
     return None, None
 
 
-def cpu_baseline(X, g0, iters, d_full):
-    """Time the oracle gm2 (PyTorch CPU, op-for-op the reference) on a sample."""
+def fixed_point_step(X: torch.Tensor, g: torch.Tensor, allreduce=None, rows=64):
+    """fp64 Weiszfeld step at g over this rank's columns (all ranks' sums combined by
+    `allreduce`): returns (||T(g) - g||, ||g||) with T the gm2 map (M:174-179).  At a
+    converged aggregate ||T(g) - g|| is of the order of the reference's last movement
+    (<= tol = 1e-5); a wrong aggregate shows up as a large step."""
+    K = X.shape[0]
+    gd = g.double()
+    d2 = torch.zeros(K, dtype=torch.float64, device=X.device)
+    for k0 in range(0, K, rows):
+        d2[k0:k0 + rows] = ((X[k0:k0 + rows].double() - gd) ** 2).sum(1)
+    if allreduce:
+        allreduce(d2)
+    w = 1.0 / d2.sqrt().clamp_min(1e-4)
+    step = torch.zeros_like(gd)
+    for k0 in range(0, K, rows):
+        step += (w[k0:k0 + rows, None] * (X[k0:k0 + rows].double() - gd)).sum(0)
+    step /= w.sum()
+    nums = torch.stack([(step ** 2).sum(), (gd ** 2).sum()])
+    if allreduce:
+        allreduce(nums)
+    return math.sqrt(float(nums[0])), math.sqrt(float(nums[1]))
+
+
+def cpu_baseline(X, g0, agg, var, iters, d_full, budget, max_cols):
+    """Time the CPU oracle (op-for-op torch-CPU restatement of the reference's gm2 /
+    gm, M:131-184) on a bounded sample of the same matrix: the first `max_cols`
+    columns, a fixed iteration count (tol disabled), scaled to the full
+    aggregation (iters Weiszfeld iterations over d_full columns)."""
     from oracle import aggregators as orc
-    threads = torch.get_num_threads()
-    Xc, gc = X.cpu(), g0.cpu()
-    t0 = time.perf_counter()
-    _, tr = orc.gm2(Xc, {"maxiter": iters, "tol": -1.0, "guess": gc})
-    dt = time.perf_counter() - t0
-    K, d = Xc.shape
-    per_agg_full = dt * (d_full / d)
+    threads = host_cpu_share()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        dc = min(max_cols, X.shape[1])
+        Xc, gc = X[:, :dc].contiguous().cpu(), g0[:dc].contiguous().cpu()
+        fn = (lambda n: orc.gm2(Xc, {"maxiter": n, "tol": -1.0, "guess": gc})) if agg == "gm2" \
+            else (lambda n: orc.gm(Xc, {"maxiter": n, "tol": -1.0, "guess": gc, "noise_var": var,
+                                        "P_max": 1}))
+        t0 = time.perf_counter()
+        fn(1)
+        t1 = time.perf_counter() - t0
+        n = max(1, min(iters - 1, int(budget / max(t1, 1e-6))))
+        t0 = time.perf_counter()
+        fn(n)
+        tn = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    per_iter = tn / n
+    per_agg_full = per_iter * iters * (d_full / dc)
+    K = X.shape[0]
     return {"value": 1.0 / per_agg_full, "unit": "aggregations/s", "cores": threads,
-            "kind": "port",
-            "sample": (f"oracle gm2 (torch CPU, {threads} threads) on the first {d} columns "
-                       f"of the same K={K} matrix, {iters} Weiszfeld iterations (the GPU's "
-                       f"converged count; tol disabled), {dt:.2f} s, extrapolated linearly "
-                       f"in d to {d_full}")}
+            "kind": "port", "ms_per_iteration_sample": 1e3 * per_iter,
+            "host_cpus_visible": os.cpu_count(),
+            "sample": (f"oracle {agg} (torch CPU, {threads} threads = this host's CPU share; "
+                       f"os.cpu_count() = {os.cpu_count()}) on the first {dc} columns of the same "
+                       f"K={K} matrix: {n} Weiszfeld iterations (tol disabled) in {tn:.2f} s; "
+                       f"scaled to {iters} iterations (the GPU's count) and d={d_full}"
+                       + ("" if dc == d_full else ", linear in d (extrapolated)"))}
 
 
 def main():
@@ -131,38 +198,49 @@ def main():
     os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    dist_path = world > 1 or args.dist
+    dist_path = world > 1 or args.dist or args.one_gpu
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     import byzantine_aircomp_amd as bz
     from byzantine_aircomp_amd import _lib
 
-    K, d_total, B = WORKLOADS[args.workload]
+    K, d_total, B, agg_name, var = WORKLOADS[args.workload]
+    agg_name = args.agg or agg_name
+    if args.var is not None:
+        var = args.var
     if args.rehearse_shard and (world != 1 or not args.dist):
         raise SystemExit("--rehearse-shard needs --dist at world size 1")
-    lo, hi = shard_range(d_total, args.rehearse_shard or world, rank)
-    d = hi - lo
-    ctx = bz.context(dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    sg = None
+    allreduce = None
     if dist_path:
         import torch.distributed as dist
+        from byzantine_aircomp_amd.sharded import ShardedGM, shard_range
         for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29533"), ("RANK", "0"),
                      ("WORLD_SIZE", "1")):
             os.environ.setdefault(k, v)      # plain `python bench.py --dist` (rehearsal)
-        dist.init_process_group("nccl", device_id=dev)
-        ctx.set_shard(d_total, lo)
-        uid = [None]
-        if rank == 0:
-            import ctypes as C
-            buf = C.create_string_buffer(128)
-            _lib.check(ctx.lib.gm_rccl_get_unique_id(buf), "gm_rccl_get_unique_id")
-            uid[0] = buf.raw
-        dist.broadcast_object_list(uid, src=0)
-        ctx.init_rccl(uid[0], world, rank)
+        if args.one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+        shard = shard_range(d_total, args.rehearse_shard, 0) if args.rehearse_shard else None
+        # the aggregation's own context (RCCL comm + this rank's shard), never the
+        # process-wide per-device one
+        sg = ShardedGM(d_total, device=dev, transport="torch" if args.one_gpu else "rccl",
+                       shard=shard)
+        ctx = sg.ctx
+        lo, hi = sg.lo, sg.hi
 
-    stream = torch.cuda.current_stream(dev).cuda_stream
+        def allreduce(t):
+            dist.all_reduce(t)
+    else:
+        ctx = bz.context(dev)
+        lo, hi = 0, d_total
+    d = hi - lo
+
     X = torch.empty(K, d, dtype=torch.float32, device=dev)
     _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, X.data_ptr(), K, d, d, B, 0.0, 0.05, 0.25,
                                            0.5, 20211, stream), "fill")
@@ -170,9 +248,18 @@ def main():
     _lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), d, 0.0, 0.01, 20212, stream),
                "fill")
     opts = {"maxiter": args.maxiter, "tol": 1e-5, "guess": g0, "algo": args.algo}
-    if args.agg == "gm":
-        opts.update(noise_var=args.var, seed=2021)
-    agg = bz.gm2 if args.agg == "gm2" else bz.gm
+    if agg_name == "gm":
+        opts.update(noise_var=var, seed=2021)
+    if sg is not None:
+        agg = sg.gm2 if agg_name == "gm2" else sg.gm
+
+        def last():
+            return sg.last_result
+    else:
+        agg = bz.gm2 if agg_name == "gm2" else bz.gm
+
+        def last():
+            return bz.aggregators.last_result
     layout = args.layout
     if layout == "auto":
         layout = "panels" if args.workload.startswith("c3") and args.algo in ("auto", "stream") \
@@ -189,7 +276,7 @@ def main():
 
     def measure(Xin, steps, warmup):
         """warmup untimed aggregations, then `steps` timed between barriers +
-        device syncs; returns (max-over-ranks seconds, pass ms, launches, result)."""
+        device syncs; returns (max-over-ranks seconds, pass ms, launches, result, out)."""
         for _ in range(warmup):
             agg(Xin, opts)
         torch.cuda.synchronize(dev)
@@ -205,35 +292,53 @@ def main():
             torch.distributed.barrier()
         t1 = time.perf_counter()
         pass_ms, launches = ctx.pass_timing(False)
-        res = bz.aggregators.last_result
+        res = last()
         elapsed = t1 - t0
         if dist_path:
-            t = torch.tensor([elapsed], device=dev)
+            t = torch.tensor([elapsed], dtype=torch.float64,
+                             device="cpu" if args.one_gpu else dev)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             elapsed = float(t.item())
-        del out
-        return elapsed, pass_ms, launches, res
+        return elapsed, pass_ms, launches, res, out
 
-    elapsed, pass_ms, launches, res = measure(inputs(layout), args.steps, args.warmup)
+    elapsed, pass_ms, launches, res, out = measure(inputs(layout), args.steps, args.warmup)
+    passes = 2 if res.algo.startswith("gram") else res.iters + 1
     alt = None
     alt_layout = "rows" if layout == "panels" else "panels"
     alt_steps = args.alt_steps if args.alt_steps is not None else max(3, args.steps // 4)
     if alt_steps > 0 and (alt_layout == "rows" or (args.algo in ("auto", "stream")
-                                                   and bz.panel_width(K) > 0)):
-        a_el, a_ms, a_n, a_res = measure(inputs(alt_layout), alt_steps, 1)
+                                                   and bz.panel_width(K) > 0
+                                                   and d_total >= 1 << 20)):
+        a_el, a_ms, a_n, a_res, _ = measure(inputs(alt_layout), alt_steps, 1)
         a_pass = (a_ms / 1e3) / max(a_n, 1)
+        a_passes = 2 if a_res.algo.startswith("gram") else a_res.iters + 1
         alt = {"layout": alt_layout, "value": alt_steps / a_el, "steps": alt_steps,
                "ms_per_step": 1e3 * a_el / alt_steps, "iters": a_res.iters, "algo": a_res.algo,
                "avg_launch_us": a_pass * 1e6,
-               "frac": 4.0 * K * d / a_pass / 1e9 / HBM_PEAK_GBS}
-    if panels is not None and layout == "rows":
-        panels = None
+               "frac": 4.0 * K * d / a_pass / 1e9 / HBM_PEAK_GBS,
+               "aggregation_frac": a_passes * 4.0 * K * d / (a_el / alt_steps) / 1e9
+               / HBM_PEAK_GBS}
+    panels = None
+
+    # full-size correctness: the fp64 fixed-point step at the returned aggregate
+    check = None
+    if not args.no_check and agg_name == "gm2":
+        step, gn = fixed_point_step(X, out, allreduce)
+        check = {"what": "fp64 gm2 step ||T(g) - g|| at the returned g over the full K x d "
+                         "(T = M:174-179); the reference stops at movement <= tol = 1e-5",
+                 "fixed_point_step": step, "g_norm": gn, "relative": step / max(gn, 1e-300),
+                 "last_movement": res.last_movement, "ok": step <= 1e-4}
+    elif not args.no_check:
+        check = {"what": "gm (AirComp) never converges (fresh channel draw each iteration, "
+                         "SURVEY §3C); parity is pinned by tests/test_gpu_weiszfeld.py",
+                 "iters": res.iters, "finite": bool(torch.isfinite(out).all())}
 
     if rank == 0:
         per_launch_bytes = 4.0 * K * d
         avg_pass_s = (pass_ms / 1e3) / max(launches, 1)
         achieved = per_launch_bytes / avg_pass_s / 1e9
-        traffic, traffic_src = pmc_traffic(args.workload, layout) if world == 1 else (None, None)
+        agg_s = elapsed / args.steps
+        agg_frac = passes * per_launch_bytes / agg_s / 1e9 / HBM_PEAK_GBS
         if res.algo in ("gram", "gram_f32"):
             # dominant kernel = the Gram partial: upper-triangle 32x32 tiles of the
             # K-padded Gram, 2 FLOP per MAC, d_local columns; the split kernel issues
@@ -245,27 +350,61 @@ def main():
             peak = MFMA_BF16_PEAK_TFLOPS if split else MFMA_F32_PEAK_TFLOPS
             tf = flops / avg_pass_s / 1e12
             gbs = per_launch_bytes / avg_pass_s / 1e9
+            traffic, traffic_src = pmc_traffic(args.workload, layout, "gram_split_partial") \
+                if world == 1 and split else (None, None)
             mf = {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s",
-                  "frac": tf / peak, "traffic": None}
+                  "frac": tf / peak, "traffic": traffic}
             hb = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                  "frac": gbs / HBM_PEAK_GBS, "traffic": None}
+                  "frac": gbs / HBM_PEAK_GBS, "traffic": traffic}
             roof, other = (mf, hb) if mf["frac"] >= hb["frac"] else (hb, mf)
             roof.update({"kernel": ("gram_split_partial (v_mfma_f32_32x32x16_bf16, h+m split, "
                                     "upper-triangle tiles)") if split else
                                    "gram_partial (v_mfma_f32_32x32x2_f32, upper-triangle tiles)",
+                         "traffic_unit": "GB per launch", "traffic_source": traffic_src,
                          "launches_timed": launches, "avg_launch_us": avg_pass_s * 1e6,
                          "algorithmic_flops_per_launch": flops,
                          "algorithmic_bytes_per_launch": per_launch_bytes,
-                         "other_ceiling": other})
+                         "other_ceiling": other,
+                         "aggregation_frac": agg_frac,
+                         "aggregation_frac_def": "2 reads of X (Gram + closing pass) x 4*K*d_local "
+                                                 "/ ms_per_step / 8 TB/s"})
+        elif res.algo == "resident":
+            # one cooperative launch runs the whole aggregation with X held in VGPRs
+            # (resident.hip): price its algorithmic bytes as 4*K*d per pass over the
+            # iterations it ran; the matrix (1.57 MB at C2) lives in registers, so this is a
+            # latency-bound kernel and the HBM fraction says how far from streaming it is
+            bytes_agg = per_launch_bytes * passes
+            gbs = bytes_agg / avg_pass_s / 1e9
+            roof = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+                    "kernel": "weiszfeld_resident (every iteration in one cooperative launch)",
+                    "launches_timed": launches, "avg_launch_us": avg_pass_s * 1e6,
+                    "us_per_iteration": avg_pass_s * 1e6 / max(res.iters, 1),
+                    "algorithmic_bytes_per_launch": bytes_agg,
+                    "aggregation_frac": agg_frac,
+                    "note": "X (K*d*4 bytes) is read from HBM once per launch and kept in "
+                            "registers; the per-iteration cost is the grid barrier + K-space step"}
         else:
+            traffic, traffic_src = pmc_traffic(args.workload, layout) if world == 1 \
+                else (None, None)
             roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                     "traffic_unit": "GB per launch", "traffic_source": traffic_src,
                     "kernel": f"weiszfeld_pass (STEP, {layout})", "launches_timed": launches,
                     "avg_launch_us": avg_pass_s * 1e6,
-                    "algorithmic_bytes_per_launch": per_launch_bytes}
+                    "algorithmic_bytes_per_launch": per_launch_bytes,
+                    "aggregation_frac": agg_frac,
+                    "aggregation_frac_def": "4*K*d_local*(iters+1) / ms_per_step / 8 TB/s "
+                                            "(BASELINE.md §3)"}
+        if dist_path and not args.rehearse_shard and world > 1:
+            parallelism = f"d-shard x{world}" + (" (one-GPU gloo rehearsal)" if args.one_gpu else "")
+        elif args.rehearse_shard:
+            parallelism = (f"rehearsal: rank 0 of a d-shard x{args.rehearse_shard} job on 1 GPU "
+                           f"(d_local {d})")
+        else:
+            parallelism = "d-shard x1 (process group)" if dist_path else "none"
         line = {
-            "metric": "GM aggregations/sec at K=1000,d=11M; % HBM roofline; 1/2/4/8 GPUs",
+            "metric": METRIC,
             "value": args.steps / elapsed,
             "unit": "aggregations/s",
             "n_gpus": world,
@@ -278,26 +417,24 @@ def main():
             "dtype": "f32",
             "data": "synthetic (Philox on device: honest N(0,0.05^2), last 20% N(0.25,0.5^2), "
                     "guess N(0,0.01^2))",
-            "config": {"workload": f"{args.workload}: {args.agg} K={K} x d={d_total} fp32, B={B} "
+            "config": {"workload": f"{args.workload}: {agg_name} K={K} x d={d_total} fp32, B={B} "
                                    f"Byzantine, tol 1e-5, maxiter {args.maxiter}"
-                                   + (f", noise_var {args.var}" if args.agg == "gm" else ""),
-                       "K": K, "d": d_total, "byzantine": B, "iters": res.iters,
-                       "algo": res.algo, "layout": layout,
-                       "parallelism": (f"rehearsal: rank 0 of a d-shard x{args.rehearse_shard} "
-                                       f"job on 1 GPU (d_local {d})" if args.rehearse_shard else
-                                       f"d-shard x{world}" if dist_path else "none"),
-                       "passes_per_aggregation": 2 if res.algo.startswith("gram") else res.iters + 1},
+                                   + (f", noise_var {var}" if agg_name == "gm" else ""),
+                       "K": K, "d": d_total, "d_local": d, "byzantine": B, "iters": res.iters,
+                       "algo": res.algo, "gram_guard": res.guard, "layout": layout,
+                       "parallelism": parallelism, "passes_per_aggregation": passes},
             "roofline": roof,
             "cpu_baseline": None,
+            "check": check,
             "alt_layout": alt,
         }
-        if world == 1 and not args.no_cpu and args.agg == "gm2":
-            dc = min(args.cpu_d, d)
-            line["cpu_baseline"] = cpu_baseline(X[:, :dc].contiguous(), g0[:dc], res.iters, d_total)
+        if world == 1 and not args.no_cpu and not args.rehearse_shard:
+            line["cpu_baseline"] = cpu_baseline(X, g0, agg_name, var, res.iters, d_total,
+                                                args.cpu_budget, args.cpu_d)
         print(json.dumps(line), file=json_out, flush=True)
     torch.cuda.synchronize(dev)
-    ctx.close()                       # RCCL communicator + workspace, before the process group
-    if dist_path:
+    if sg is not None:
+        sg.close()                    # RCCL communicator + workspace, before the process group
         torch.distributed.destroy_process_group()
 
 

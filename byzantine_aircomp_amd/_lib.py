@@ -12,13 +12,14 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMAGG_LIB", os.path.join(HERE, "libgmagg.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 GM_MODE_IDEAL, GM_MODE_AIRCOMP = 0, 1
 GM_NOISE_PHILOX, GM_NOISE_HOST = 0, 1
 GM_ALGO_AUTO, GM_ALGO_STREAM, GM_ALGO_TWOPASS, GM_ALGO_GRAM, GM_ALGO_RESIDENT = 0, 1, 2, 3, 4
 GM_ALGO_GRAM_F32 = 5
 GM_LAYOUT_ROWS, GM_LAYOUT_PANELS = 0, 1
+GM_GUARD_NONE, GM_GUARD_ACCEPTED, GM_GUARD_REJECTED = 0, 1, 2
 
 NOISE_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.POINTER(C.c_float),
                        C.POINTER(C.c_float), C.POINTER(C.c_float))
@@ -50,6 +51,8 @@ class GmResult(C.Structure):
         ("last_movement", C.c_double),
         ("converged", C.c_int32),
         ("algo_used", C.c_int32),
+        ("guard", C.c_int32),
+        ("reserved", C.c_int32),
     ]
 
 

@@ -55,6 +55,7 @@ class GMResult:
     last_movement: float
     converged: bool
     algo: str
+    guard: str = "none"      # Gram accuracy guard: "none", "accepted", "rejected"
 
 
 last_result: GMResult | None = None
@@ -62,6 +63,13 @@ _ALGOS = {"auto": _lib.GM_ALGO_AUTO, "stream": _lib.GM_ALGO_STREAM,
           "twopass": _lib.GM_ALGO_TWOPASS, "gram": _lib.GM_ALGO_GRAM,
           "resident": _lib.GM_ALGO_RESIDENT, "gram_f32": _lib.GM_ALGO_GRAM_F32}
 _ALGO_NAMES = {v: k for k, v in _ALGOS.items()}
+_GUARD_NAMES = {_lib.GM_GUARD_NONE: "none", _lib.GM_GUARD_ACCEPTED: "accepted",
+                _lib.GM_GUARD_REJECTED: "rejected"}
+
+
+def _result(res) -> "GMResult":
+    return GMResult(res.iters, res.last_movement, bool(res.converged),
+                    _ALGO_NAMES.get(res.algo_used, "?"), _GUARD_NAMES.get(res.guard, "?"))
 
 
 class Context:
@@ -248,8 +256,7 @@ def _weiszfeld(wList: torch.Tensor, options: dict, aircomp: bool):
         _lib.check(ctx.lib.gm_weiszfeld_f32(ctx.handle, X.data_ptr(), K, d, ldx, g0.data_ptr(),
                                             out.data_ptr(), C.byref(o), C.byref(res),
                                             _stream_ptr(X.device)), "gm_weiszfeld_f32")
-    last_result = GMResult(res.iters, res.last_movement, bool(res.converged),
-                           _ALGO_NAMES.get(res.algo_used, "?"))
+    last_result = _result(res)
     return out if wList.device == out.device else out.to(wList.device)
 
 

@@ -47,6 +47,7 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 }  // namespace
 
+
 struct gm_ctx {
   int device = 0;
   int num_cu = 256;
@@ -63,9 +64,36 @@ struct gm_ctx {
   hipEvent_t poll_ev[2] = {nullptr, nullptr};   // lagged convergence polls
   std::vector<hipEvent_t> ev_free;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used;
+  // Workspace ordering across streams: every call that touches ws / host records
+  // ws_ev on its stream when it returns (work may still be queued: the lagged
+  // poll returns before the no-op tail drains); a call on ANOTHER stream waits
+  // for it before zeroing or overwriting the workspace.
+  hipEvent_t ws_ev = nullptr;
+  hipStream_t ws_stream = nullptr;
+  bool ws_pending = false;
 };
 
 namespace {
+
+// Stream-orders the context's workspace between calls (see gm_ctx::ws_ev): the
+// constructor makes `s` wait for the previous call's tail when that call ran on
+// another stream; the destructor marks the end of this call's work on `s`.
+struct WsOrder {
+  gm_ctx* c;
+  hipStream_t s;
+  hipError_t err = hipSuccess;
+  WsOrder(gm_ctx* c_, hipStream_t s_) : c(c_), s(s_) {
+    if (!c->ws_ev) err = hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming);
+    if (err == hipSuccess && c->ws_pending && c->ws_stream != s)
+      err = hipStreamWaitEvent(s, c->ws_ev, 0);
+  }
+  ~WsOrder() {
+    if (c->ws_ev && hipEventRecord(c->ws_ev, s) == hipSuccess) {
+      c->ws_stream = s;
+      c->ws_pending = true;
+    }
+  }
+};
 
 struct Workspace {
   KState* st;
@@ -228,7 +256,8 @@ int record_pass_end(gm_ctx* c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
 // iteration on the device.
 int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
                  const float* guess0, float* out, const gm_opts* o, gm_result* res,
-                 const PassCfg& cfg, int nch, hipStream_t s) {
+                 const PassCfg& cfg, int nch, hipStream_t s, bool* timed_out) {
+  *timed_out = false;
   const int64_t S = 2 * K + 2;
   Workspace w;
   int rc = ensure_ws(c, K, d, (int)(2 * nch), &w);   // slab [2][nch][2K+2]
@@ -256,7 +285,15 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   unsigned hbar[4] = {0, 0, 0, 0};
   HIPCHK(hipMemcpyAsync(hbar, bar, 16, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  if (hbar[2]) return fail(GM_ERR_HIP, "resident kernel: grid barrier timed out");
+  if (hbar[2]) {   // the grid was not co-resident long enough: caller reruns on streaming
+    *timed_out = true;
+    if (c->timing && !c->ev_used.empty()) {
+      c->ev_free.push_back(c->ev_used.back().first);
+      c->ev_free.push_back(c->ev_used.back().second);
+      c->ev_used.pop_back();
+    }
+    return GM_OK;
+  }
   gm_result r{};
   r.iters = hst->iters;
   r.last_movement = hst->last_movement;
@@ -355,6 +392,7 @@ int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const
   r.last_movement = hst->last_movement;
   r.converged = hst->converged;
   r.algo_used = split ? GM_ALGO_GRAM : GM_ALGO_GRAM_F32;
+  r.guard = guarded ? GM_GUARD_ACCEPTED : GM_GUARD_NONE;
   if (res) *res = r;
   return GM_OK;
 }
@@ -474,8 +512,16 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
     return fail(GM_ERR_INVALID, "gm_weiszfeld_f32: GM_NOISE_HOST needs noise_cb");
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int64_t d_total = c->d_total > 0 ? c->d_total : d;
-  const int64_t col_off = c->d_total > 0 ? c->d_offset : 0;
+  WsOrder order(c, s);
+  HIPCHK(order.err);
+  // d-sharding: every decision that changes the sequence of collectives (Gram or
+  // streaming, the poll interval and with it the passes queued after the stop) is
+  // taken from GLOBAL quantities (K, d_total, options), so all ranks issue the same
+  // all-reduces even when the last shard is shorter or ragged.  Local properties
+  // (vector width, tile) only pick kernels.
+  const bool sharded = c->d_total > 0;
+  const int64_t d_total = sharded ? c->d_total : d;
+  const int64_t col_off = sharded ? c->d_offset : 0;
   gm_result r{};
   if (o->maxiter == 0) {
     HIPCHK(hipMemcpyAsync(out, guess0, sizeof(float) * d, hipMemcpyDeviceToDevice, s));
@@ -508,11 +554,25 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   // AUTO: Gram-space (split bf16) for gm2 at K <= 256 on large d, kept if its
   // accuracy guard passes (run_gram); streaming otherwise.  X is read twice
   // instead of n+1 times (profiles/r01_cmp_algos.txt, r02_gram_split.txt).
-  if (algo == GM_ALGO_AUTO && o->mode == GM_MODE_IDEAL && gram_kt(K) > 0 && V == 4 &&
-      d >= (int64_t)1 << 18 && ldx < ((int64_t)1 << 26) && pick_cfg(K, V, ldx, &cfg)) {
+  // Sharded: the choice is made on d_total (every rank the same); each rank's
+  // shard must then meet the kernel's local needs, which shard_range-aligned,
+  // contiguous shards of a d_total % 4 == 0 update always do.
+  const bool gram_local_ok = gram_kt(K) > 0 && V == 4 && ldx < ((int64_t)1 << 26) &&
+                             pick_cfg(K, V, ldx, &cfg);
+  bool guard_rejected = false;   // a Gram result was computed and refused by the guard
+  const bool gram_auto = algo == GM_ALGO_AUTO && o->mode == GM_MODE_IDEAL && !panels &&
+                         gram_kt(K) > 0 && d_total >= (int64_t)1 << 18 &&
+                         (sharded ? d_total % 4 == 0 : gram_local_ok);
+  if (gram_auto) {
+    if (!gram_local_ok)
+      return fail(GM_ERR_INVALID, "sharded gm2 (AUTO -> Gram, d_total=%lld): this rank's shard "
+                  "must be 16-byte aligned with d_local %% 4 == 0 and ldx %% 4 == 0 like every "
+                  "other rank's (use sharded.shard_range + contiguous shards)",
+                  (long long)d_total);
     bool rejected = false;
     const int rc0 = run_gram(c, X, K, d, ldx, guess0, out, o, res, cfg, s, true, true, &rejected);
     if (rc0 || !rejected) return rc0;
+    guard_rejected = true;
   }
   // Small problems: the register-resident single launch when every chunk fits one
   // co-resident block (unsharded, Philox or no noise).
@@ -521,8 +581,15 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       c->d_total <= 0 && !c->comm && !c->ar_fn && pick_cfg(K, V, ldx, &cfg)) {
     const int J = cfg.LPR * cfg.V;
     const int64_t nch = (d + J - 1) / J;
-    if (nch <= resident_max_blocks(cfg, c->num_cu))
-      return run_resident(c, X, K, d, ldx, guess0, out, o, res, cfg, (int)nch, s);
+    if (nch <= resident_max_blocks(cfg, c->num_cu)) {
+      bool timed_out = false;
+      const int rc0 = run_resident(c, X, K, d, ldx, guess0, out, o, res, cfg, (int)nch, s,
+                                   &timed_out);
+      if (rc0 || !timed_out) return rc0;
+      // barrier timeout (e.g. a time-sliced GPU): the same problem, same draw keys,
+      // on the launch-per-pass streaming path below
+      if (algo == GM_ALGO_RESIDENT) algo = GM_ALGO_AUTO;
+    }
   }
   if (algo == GM_ALGO_RESIDENT)
     return fail(GM_ERR_UNSUPPORTED, "resident kernel: problem too large, sharded or host noise");
@@ -543,8 +610,17 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
                   (long long)ldx);
     // the split kernel addresses a 16-row group with 32-bit lane offsets
     const bool split = algo == GM_ALGO_GRAM && ldx < ((int64_t)1 << 26);
+    // Explicit Gram runs the same a-posteriori guard as AUTO: a result the guard
+    // refuses is never returned; the call then runs the streaming path and
+    // reports guard = GM_GUARD_REJECTED.  (GMAGG_GRAM_UNGUARDED=1: A/B timing of
+    // the bare Gram path, whose closing pass is the lighter sum-only tile.)
+    static const bool unguarded = getenv("GMAGG_GRAM_UNGUARDED") != nullptr;
     bool rejected = false;
-    return run_gram(c, X, K, d, ldx, guess0, out, o, res, cfg, s, split, false, &rejected);
+    const int rc0 = run_gram(c, X, K, d, ldx, guess0, out, o, res, cfg, s, split, !unguarded,
+                             &rejected);
+    if (rc0 || !rejected) return rc0;
+    guard_rejected = true;
+    algo = GM_ALGO_STREAM;   // pick_cfg(K, V, ldx) succeeded above
   }
   if (algo != GM_ALGO_STREAM && algo != GM_ALGO_TWOPASS)
     return fail(GM_ERR_INVALID, "unknown algo %d", o->algo);
@@ -653,7 +729,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   HIPCHK(launch_kspace(ka, s));
 
   int check_every = o->check_every;
-  if (check_every <= 0) check_every = (K * d >= (int64_t)1 << 24) ? 1 : 16;
+  if (check_every <= 0) check_every = (K * d_total >= (int64_t)1 << 24) ? 1 : 16;   // global
   if (host_noise) check_every = 1;
   // Polling every iteration (large passes): read iteration t-1's state while
   // iteration t is already queued, so the device never waits for the host.  If
@@ -722,6 +798,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   r.last_movement = final_st->last_movement;
   r.converged = final_st->converged;
   r.algo_used = algo;
+  r.guard = guard_rejected ? GM_GUARD_REJECTED : GM_GUARD_NONE;
   if (r.iters < 1) return fail(GM_ERR_HIP, "Weiszfeld loop recorded no iteration");
   // passes queued after the stop (lagged poll) exited at once: not timed as passes
   for (int64_t k = r.iters; k < enqueued && c->timing && !c->ev_used.empty(); ++k) {
@@ -749,10 +826,12 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
   if (c->d_total > 0) return fail(GM_ERR_UNSUPPORTED, "batched problems are not d-sharded");
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  WsOrder order(c, s);
+  HIPCHK(order.err);
   if (o->maxiter == 0) {
     HIPCHK(hipMemcpy2DAsync(out, ldo * 4, guess0, ldg * 4, d * 4, P, hipMemcpyDeviceToDevice, s));
     if (results)
-      for (int64_t p = 0; p < P; ++p) results[p] = gm_result{0, NAN, 0, GM_ALGO_STREAM};
+      for (int64_t p = 0; p < P; ++p) results[p] = gm_result{0, NAN, 0, GM_ALGO_STREAM, GM_GUARD_NONE, 0};
     return GM_OK;
   }
   PassCfg cfg{};
@@ -864,7 +943,8 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
   HIPCHK(hipStreamSynchronize(s));
   if (results)
     for (int64_t p = 0; p < P; ++p)
-      results[p] = gm_result{hst[p].iters, hst[p].last_movement, hst[p].converged, GM_ALGO_STREAM};
+      results[p] = gm_result{hst[p].iters, hst[p].last_movement, hst[p].converged, GM_ALGO_STREAM,
+                             GM_GUARD_NONE, 0};
   return GM_OK;
 }
 
@@ -904,6 +984,8 @@ int gm_krum_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, in
     return fail(GM_ERR_INVALID, "gm_krum_f32: bad args (needs 2 <= honestSize <= K+1)");
   if (K > 4096) return fail(GM_ERR_UNSUPPORTED, "gm_krum_f32: K <= 4096");
   HIPCHK(hipSetDevice(c->device));
+  WsOrder order(c, reinterpret_cast<hipStream_t>(stream));
+  HIPCHK(order.err);
   Workspace w;
   // G area holds the K x K distances; the float slab holds the per-slice fp64 partials
   const size_t part_doubles = (size_t)krum_slices(K, d) * (size_t)(K * K);

@@ -70,8 +70,10 @@ __host__ __device__ __forceinline__ void normal4(uint64_t seed, uint32_t stream,
 
 // Box-Muller on the hardware transcendentals: v_log_f32 (log2), v_sqrt_f32 and
 // v_sin/v_cos_f32, which take their argument in revolutions, so u01(b) goes in
-// unscaled.  ~1 ulp each; contraction off so every call site rounds alike (a
-// normal must come out identical whichever code path regenerates it).
+// unscaled.  ~1 ulp each; contraction off so every DEVICE call site rounds alike
+// (a normal must come out identical whichever kernel regenerates it).  Host code
+// has no equivalent: the CPU restatement (oracle/philox.py) uses libm-precision
+// Box-Muller and is compared with a tolerance, never bit for bit.
 __device__ __forceinline__ void box_muller_hw(uint32_t a, uint32_t b, float* n0, float* n1) {
 #pragma clang fp contract(off)
   const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01(a)));
@@ -90,14 +92,15 @@ __device__ __forceinline__ void normal4_hw(uint64_t seed, uint32_t stream, uint6
 }
 
 // One standard normal for element `idx` (uses half of a Philox block): the AirComp
-// column noise, drawn by the pass's finisher threads between two block barriers, so
-// the device takes the hardware Box-Muller (every device call site alike).
-__host__ __device__ __forceinline__ float normal1(uint64_t seed, uint32_t stream, uint64_t iter,
-                                                  uint64_t idx) {
+// column noise, drawn by the pass's finisher threads between two block barriers, on
+// the hardware Box-Muller.  Device-only: every call site that regenerates a draw
+// runs this same code, so a draw is identical wherever it is made.
+__device__ __forceinline__ float normal1(uint64_t seed, uint32_t stream, uint64_t iter,
+                                         uint64_t idx) {
   u4 c{(uint32_t)idx, (uint32_t)(idx >> 32), (uint32_t)iter, stream ^ (uint32_t)(iter >> 32)};
   u4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
   float n0, n1;
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(GMK_NORMAL1_PRECISE)   // A/B knob
+#ifndef GMK_NORMAL1_PRECISE   // A/B knob: libm-style Box-Muller on the device
   box_muller_hw(r.x, r.y, &n0, &n1);
 #else
   box_muller(r.x, r.y, &n0, &n1);

@@ -39,9 +39,14 @@ namespace gmk {
 
 // (ResArgs: gmagg_internal.h)
 
+constexpr uint64_t kBarrierTicks = 200000000ull;   // 2 s at the 100 MHz real-time clock
+
 // Grid barrier: arrival counter + generation word, agent-scope release before
 // arriving and acquire after leaving (cdna_hip_programming.md §6 G16).  The spin
-// is bounded: on timeout a flag is raised and every block gives up.
+// is bounded in WALL time (s_memrealtime, 100 MHz: kBarrierTicks = 2 s, so a
+// time-sliced GPU does not trip it by spinning slowly): on timeout a flag is
+// raised, every block gives up, and the host reruns the problem on the
+// streaming path (api.hip run_resident).
 __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned nblocks, unsigned& gen,
                                           int* s_ok) {
   __syncthreads();
@@ -56,11 +61,13 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned nblocks, unsig
       __hip_atomic_store(&bar[1], g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       unsigned spins = 0;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
 #if GMK_RES_SLEEP > 0
         __builtin_amdgcn_s_sleep(GMK_RES_SLEEP);
 #endif
-        if (++spins > (1u << 24) ||
+        if (((++spins & 1023u) == 0 &&
+             __builtin_amdgcn_s_memrealtime() - t0 > kBarrierTicks) ||
             __hip_atomic_load(&bar[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
           __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           ok = 0;

@@ -23,7 +23,7 @@ import ctypes as C
 import torch
 
 from . import _lib
-from .aggregators import GMResult, Context, _ALGO_NAMES, _ALGOS, _noise_source, _seed
+from .aggregators import GMResult, Context, _ALGOS, _noise_source, _result, _seed
 from .panels import ClientPanels
 
 __all__ = ["shard_range", "ShardedGM", "torch_allreduce_adapter"]
@@ -73,14 +73,24 @@ class ShardedGM:
     """gm2 / gm on this rank's column shard of a d_total-long update."""
 
     def __init__(self, d_total: int, group=None, device: torch.device | None = None,
-                 transport: str = "rccl"):
+                 transport: str = "rccl", shard: tuple[int, int] | None = None):
+        """``shard`` overrides this rank's [lo, hi) columns (default: the even
+        ``shard_range`` plan).  Every rank's shard must then start at a multiple of
+        256 columns and the shards must tile [0, d_total) — a one-GPU rehearsal of
+        rank r of a larger job passes ``shard_range(d_total, P, r)`` at world size 1."""
         import torch.distributed as dist
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.d_total = d_total
-        self.lo, self.hi = shard_range(d_total, self.world, self.rank)
+        if shard is None:
+            self.lo, self.hi = shard_range(d_total, self.world, self.rank)
+        else:
+            self.lo, self.hi = int(shard[0]), int(shard[1])
+            if not (0 <= self.lo <= self.hi <= d_total) or self.lo % ALIGN:
+                raise ValueError(f"shard {shard} of d_total={d_total}: need 0 <= lo <= hi <= "
+                                 f"d_total and lo % {ALIGN} == 0")
         self.ctx = Context(self.device.index)
         self.ctx.set_shard(d_total, self.lo)
         if transport == "rccl":
@@ -142,8 +152,7 @@ class ShardedGM:
                 self.ctx.handle, ptr, K, self.d_local, ldx,
                 g0.data_ptr(), out.data_ptr(), C.byref(o), C.byref(res),
                 torch.cuda.current_stream(self.device).cuda_stream), "gm_weiszfeld_f32")
-        self.last_result = GMResult(res.iters, res.last_movement, bool(res.converged),
-                                    _ALGO_NAMES.get(res.algo_used, "?"))
+        self.last_result = _result(res)
         return out
 
     def gm2(self, X, options=None):

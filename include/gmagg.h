@@ -17,7 +17,10 @@
  *   - Work is stream-ordered on `stream` (a hipStream_t passed as void*; NULL =
  *     the default stream).  gm_weiszfeld_f32 blocks only to learn whether the
  *     iteration has converged; the OMA entry points never block.
- *   - A context is used by one host thread at a time.
+ *   - A context is used by one host thread at a time.  Calls on one context may
+ *     use different streams: each call makes its stream wait for the previous
+ *     call's queued work on the context's workspace (an event), so they never
+ *     race; for concurrent aggregations use one context per stream.
  *
  * Layout: X is row-major [K][ldx] fp32, row k = client k's flattened update
  * (model.parameters() order, MNIST_Air_weight.py:206-209), ldx >= d — the
@@ -36,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GMAGG_ABI_VERSION 1
+#define GMAGG_ABI_VERSION 2
 
 enum gm_status {
     GM_OK = 0,
@@ -102,11 +105,19 @@ typedef struct gm_opts {
     int32_t layout;           /* gm_layout of X (gm_weiszfeld_f32 only; batched: ROWS) */
 } gm_opts;
 
+enum gm_guard {
+    GM_GUARD_NONE = 0,        /* no Gram result was involved */
+    GM_GUARD_ACCEPTED = 1,    /* Gram-space result, a-posteriori accuracy guard passed */
+    GM_GUARD_REJECTED = 2     /* a Gram result was refused; the streaming path produced out */
+};
+
 typedef struct gm_result {
     int64_t iters;            /* Weiszfeld loop bodies executed (M:145 / M:173) */
     double last_movement;     /* ||guess_t - guess_{t+1}|| of the last body (M:156 / M:180) */
     int32_t converged;        /* 1 if the loop exited through the tol test */
     int32_t algo_used;        /* gm_algo actually run */
+    int32_t guard;            /* gm_guard: what the Gram accuracy guard decided */
+    int32_t reserved;
 } gm_result;
 
 typedef struct gm_ctx gm_ctx;
@@ -116,7 +127,14 @@ int gm_ctx_create(int device, gm_ctx** out);
 int gm_ctx_destroy(gm_ctx* ctx);
 
 /* d-sharding: this shard holds global columns [d_offset, d_offset + d_local) of
- * a d_total-long update; per-iteration partial sums go through the all-reduce. */
+ * a d_total-long update; per-iteration partial sums go through the all-reduce.
+ * Every rank must pass the same K, d_total and options; the library takes every
+ * decision that changes the sequence of collectives (Gram or streaming, the poll
+ * interval) from those global values, so a shorter or ragged last shard issues
+ * exactly the all-reduces the others do.  For AUTO's Gram choice (gm2, K <= 256,
+ * d_total >= 2^18, d_total % 4 == 0) each shard must also be 16-byte aligned with
+ * d_local and ldx multiples of 4 — always true for contiguous shards cut at
+ * 256-column boundaries (byzantine_aircomp_amd.sharded.shard_range). */
 int gm_ctx_set_shard(gm_ctx* ctx, int64_t d_total, int64_t d_offset);
 int gm_ctx_set_allreduce(gm_ctx* ctx, gm_allreduce_cb fn, void* user);
 /* Native RCCL all-reduce over xGMI: `unique_id` is the 128-byte ncclUniqueId

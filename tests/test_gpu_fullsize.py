@@ -1,0 +1,155 @@
+"""The kernels that produce the bench headlines, pinned to the oracle, and the
+benchmarked sizes themselves checked for correctness.
+
+* K = 1000 (the C3 tile: (NW 8, LPR 8, R 16, OCC 2), V = 4, rolling-prefetch
+  STEP) on row-major and panel inputs against oracle.gm2 at d = 65,536, where
+  the CPU oracle finishes in about a second;
+* AirComp gm at K = 1000 x 8,192 with the reference's own draws replayed
+  (host noise), 20 iterations, against oracle.gm;
+* the full C3 input (1000 x 11M, panels, as bench.py runs it) and the full C4
+  shard (256 x 15.6M, AUTO -> guarded Gram): the returned aggregate is a
+  Weiszfeld fixed point — the fp64 step ||T(g) - g|| at g (T = M:174-179) is of
+  the order of the reference's stopping movement (tol = 1e-5).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_l2
+from oracle import aggregators as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def bz():
+    import byzantine_aircomp_amd as m
+    return m
+
+
+def _fill(K, d, B, seed=20211):
+    m = bz()
+    ctx = m.context()
+    s = torch.cuda.current_stream().cuda_stream
+    X = torch.empty(K, d, device="cuda")
+    m._lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, X.data_ptr(), K, d, d, B, 0.0, 0.05, 0.25,
+                                             0.5, seed, s), "fill")
+    g0 = torch.empty(d, device="cuda")
+    m._lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), d, 0.0, 0.01, seed + 1, s),
+                 "fill")
+    return X, g0
+
+
+def _fixed_point_step(X, g, rows=64):
+    """(||T(g) - g||, ||g||) in fp64, T the gm2 map (same as bench.fixed_point_step)."""
+    K = X.shape[0]
+    gd = g.double()
+    d2 = torch.zeros(K, dtype=torch.float64, device=X.device)
+    for k0 in range(0, K, rows):
+        d2[k0:k0 + rows] = ((X[k0:k0 + rows].double() - gd) ** 2).sum(1)
+    w = 1.0 / d2.sqrt().clamp_min(1e-4)
+    step = torch.zeros_like(gd)
+    for k0 in range(0, K, rows):
+        step += (w[k0:k0 + rows, None] * (X[k0:k0 + rows].double() - gd)).sum(0)
+    step /= w.sum()
+    return float(step.norm()), float(gd.norm())
+
+
+@pytest.mark.parametrize("layout", ["rows", "panels"])
+def test_c3_tile_matches_oracle(layout):
+    K, d = 1000, 65_536
+    X, g0 = _fill(K, d, 200)
+    opts = {"maxiter": 1000, "tol": 1e-5}
+    want, tr = orc.gm2(X.cpu(), dict(opts, guess=g0.cpu()))
+    Xin = bz().ClientPanels.from_rows(X) if layout == "panels" else X
+    ctx = bz().context()
+    ctx.pass_timing(True)
+    got = bz().gm2(Xin, dict(opts, guess=g0))
+    torch.cuda.synchronize()
+    _, launches = ctx.pass_timing(False)
+    res = bz().aggregators.last_result
+    assert res.algo == "stream" and launches == res.iters
+    assert rel_l2(got.cpu().numpy(), want.numpy()) <= 1e-5
+    assert abs(res.iters - tr.iters) <= 1
+
+
+def test_c3_tile_gm_host_draws_matches_oracle():
+    """AirComp gm on the K = 1000 tile with the reference's torch.normal draws
+    (M:401-402, M:411) replayed: 20 iterations, identical count."""
+    K, d = 1000, 8192
+    X, g0 = _fill(K, d, 200, seed=99)
+    opts = {"maxiter": 20, "tol": 1e-5, "noise_var": 1e-2, "P_max": 1}
+    torch.manual_seed(2021)
+    want, tr = orc.gm(X.cpu(), dict(opts, guess=g0.cpu()))
+    torch.manual_seed(2021)
+    got = bz().gm(X, dict(opts, guess=g0, noise_source="host", algo="stream"))
+    res = bz().aggregators.last_result
+    assert res.iters == tr.iters == 20
+    assert rel_l2(got.cpu().numpy(), want.numpy()) <= 1e-5
+
+
+def test_c3_full_size_panels_fixed_point():
+    """The bench's C3 input exactly: 1000 x 11M, ClientPanels, AUTO."""
+    m = bz()
+    K, d = 1000, 11_000_000
+    X, g0 = _fill(K, d, 200)
+    P = m.ClientPanels.from_rows(X)
+    g = m.gm2(P, {"maxiter": 1000, "tol": 1e-5, "guess": g0})
+    res = m.aggregators.last_result
+    del P
+    assert res.algo == "stream" and res.converged and 2 <= res.iters <= 20
+    assert res.last_movement <= 1e-5
+    step, gn = _fixed_point_step(X, g)
+    assert math.isfinite(step) and step <= 1e-4, (step, gn)
+
+
+def test_c4_shard_full_size_gram_fixed_point():
+    """One GPU's C4 shard exactly: 256 x 15.625M, AUTO -> guarded split-bf16 Gram."""
+    m = bz()
+    K, d = 256, 15_625_000
+    X, g0 = _fill(K, d, 51)
+    g = m.gm2(X, {"maxiter": 1000, "tol": 1e-5, "guess": g0})
+    res = m.aggregators.last_result
+    assert res.algo == "gram" and res.guard == "accepted" and res.converged
+    step, gn = _fixed_point_step(X, g)
+    assert math.isfinite(step) and step <= 1e-4, (step, gn)
+    # and the streaming path agrees with it at full size
+    s = m.gm2(X, {"maxiter": 1000, "tol": 1e-5, "guess": g0, "algo": "stream"})
+    assert abs(m.aggregators.last_result.iters - res.iters) <= 1
+    assert rel_l2(g.cpu().numpy(), s.cpu().numpy()) <= 1e-5
+
+
+def test_explicit_gram_is_guarded():
+    """algo='gram' on data the guard refuses (reference movement floor above tol/3):
+    the result comes from the streaming path and says so."""
+    g = torch.Generator().manual_seed(11)
+    K, d = 64, 1 << 18
+    X = 3.0 + 0.05 * torch.randn(K, d, generator=g)
+    p = torch.zeros(d)
+    opts = {"maxiter": 30, "tol": 1e-5, "guess": p}
+    want, tr = orc.gm2(X.clone(), dict(opts))
+    got = bz().gm2(X.cuda(), dict(opts, guess=p.cuda(), algo="gram"))
+    res = bz().aggregators.last_result
+    assert res.algo == "stream" and res.guard == "rejected"
+    assert rel_l2(got.cpu().numpy(), want.numpy()) <= 1e-5
+
+
+def test_workspace_ordered_across_streams():
+    """Back-to-back calls on two streams share the context's workspace: the second
+    waits for the first's queued tail (lagged poll), so both results are exact."""
+    m = bz()
+    K, d = 1000, 1 << 16
+    X, g0 = _fill(K, d, 200, seed=5)
+    Y, h0 = _fill(K, d, 200, seed=6)
+    ref_x = m.gm2(X, {"maxiter": 1000, "guess": g0, "check_every": 1})
+    ref_y = m.gm2(Y, {"maxiter": 1000, "guess": h0, "check_every": 1})
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(3):
+        with torch.cuda.stream(s1):
+            a = m.gm2(X, {"maxiter": 1000, "guess": g0, "check_every": 1})
+        with torch.cuda.stream(s2):
+            b = m.gm2(Y, {"maxiter": 1000, "guess": h0, "check_every": 1})
+        torch.cuda.synchronize()
+        assert torch.equal(a, ref_x) and torch.equal(b, ref_y)

@@ -33,7 +33,7 @@ def _sharded(X, p, P, opts, aircomp, check_every=0, algo=0, panels=False):
 
     K, d = X.shape
     dev = X.device
-    barrier = threading.Barrier(P)
+    barrier = threading.Barrier(P, timeout=60)   # a rank-dependent collective count fails here
     bufs = [None] * P
     out = [None] * P
     errs = []
@@ -159,7 +159,10 @@ def test_sharded_gram_equals_unsharded(algo):
     from byzantine_aircomp_amd import _lib
     K, P = 64, 2
     d = 2 * (1 << 18) + 4096
-    X, p = _problem(K, d, 12, seed=21)
+    g = torch.Generator().manual_seed(21)         # C4 recipe: the guard keeps the Gram result
+    X = 0.05 * torch.randn(K, d, generator=g)
+    X[K - 12:] = 0.25 + 0.5 * torch.randn(12, d, generator=g)
+    X, p = X.cuda(), (0.01 * torch.randn(d, generator=g)).cuda()
     opts = {"maxiter": 1000, "tol": 1e-5}
     want = bz.gm2(X, dict(opts, guess=p, algo="stream"))
     n = bz.aggregators.last_result.iters
@@ -216,3 +219,32 @@ def test_oma_philox_shard_invariant(cuts):
         torch.cuda.synchronize()
         assert torch.equal(part, full[:, lo:hi]), (lo, hi)
         ctx.close()
+
+
+@pytest.mark.parametrize("K,d,P,algo,want_algo", [
+    # 1000 x 50002 over 3: shards 16896 / 16896 / 16210 columns (last ragged, d % 4 = 2);
+    # K * d_local straddles the 2^24 poll threshold, K * d_total does not
+    (1000, 50_002, 3, 0, {1}),
+    (1000, 50_002, 3, 1, {1}),
+    # d_total >= 2^18 with every shard below it: AUTO takes Gram on d_total (all ranks)
+    (200, (1 << 18) + 1024, 3, 0, {3}),
+    # d_total % 4 == 2: no Gram anywhere, although the first shards are float4-aligned
+    (200, (1 << 18) + 1026, 3, 0, {1}),
+])
+def test_sharded_ragged_last_shard_same_decisions(K, d, P, algo, want_algo):
+    """Every rank must issue the same sequence of all-reduces: the
+    Gram/streaming choice and the poll interval come from K, d_total and the
+    options, never from the local slice."""
+    import byzantine_aircomp_amd as bz
+    g = torch.Generator().manual_seed(d % 1000)    # the C3/C4 recipe (BASELINE.md §3)
+    B = K // 5
+    X = 0.05 * torch.randn(K, d, generator=g)
+    X[K - B:] = 0.25 + 0.5 * torch.randn(B, d, generator=g)
+    X, p = X.cuda(), (0.01 * torch.randn(d, generator=g)).cuda()
+    opts = {"maxiter": 1000, "tol": 1e-5}
+    want = bz.gm2(X, dict(opts, guess=p, algo="stream"))
+    n = bz.aggregators.last_result.iters
+    got, iters = _sharded(X, p, P, opts, aircomp=False, algo=algo)
+    assert len(iters) == 1 and abs(iters.pop() - n) <= 1
+    assert _sharded.algos == want_algo
+    assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-5
