@@ -52,7 +52,7 @@ class GmResult(C.Structure):
         ("converged", C.c_int32),
         ("algo_used", C.c_int32),
         ("guard", C.c_int32),
-        ("reserved", C.c_int32),
+        ("gram_kind", C.c_int32),
     ]
 
 

@@ -56,6 +56,7 @@ class GMResult:
     converged: bool
     algo: str
     guard: str = "none"      # Gram accuracy guard: "none", "accepted", "rejected"
+    gram_kind: str = ""      # Gram runs: "f16_split", "bf16_split" (f16 range fallback), "f32"
 
 
 last_result: GMResult | None = None
@@ -69,7 +70,8 @@ _GUARD_NAMES = {_lib.GM_GUARD_NONE: "none", _lib.GM_GUARD_ACCEPTED: "accepted",
 
 def _result(res) -> "GMResult":
     return GMResult(res.iters, res.last_movement, bool(res.converged),
-                    _ALGO_NAMES.get(res.algo_used, "?"), _GUARD_NAMES.get(res.guard, "?"))
+                    _ALGO_NAMES.get(res.algo_used, "?"), _GUARD_NAMES.get(res.guard, "?"),
+                    {1: "f16_split", 2: "bf16_split", 3: "f32"}.get(res.gram_kind, ""))
 
 
 class Context:

@@ -256,28 +256,32 @@ int record_pass_end(gm_ctx* c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
 // iteration on the device.
 int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
                  const float* guess0, float* out, const gm_opts* o, gm_result* res,
-                 const PassCfg& cfg, int nch, hipStream_t s, bool* timed_out) {
+                 const PassCfg& cfg, int cpb, int nb, hipStream_t s, bool* timed_out) {
   *timed_out = false;
+  // granules [2][nb][2 values] in the slab region, + the timeout word in sums
+  const size_t words = resident_gran_words(K, cfg, nb);
   const int64_t S = 2 * K + 2;
   Workspace w;
-  int rc = ensure_ws(c, K, d, (int)(2 * nch), &w);   // slab [2][nch][2K+2]
+  int rc = ensure_ws(c, K, d, (int)((words + S - 1) / S), &w);
   if (rc) return rc;
   rc = ensure_host(c, sizeof(KState));
   if (rc) return rc;
-  unsigned* bar = reinterpret_cast<unsigned*>(w.sums);  // reuse: 3 words, zeroed per call
+  unsigned* bar = reinterpret_cast<unsigned*>(w.sums);  // reuse: timeout word, zeroed per call
   HIPCHK(hipMemsetAsync(w.st, 0, sizeof(KState), s));
   HIPCHK(hipMemsetAsync(bar, 0, 16, s));
+  HIPCHK(hipMemsetAsync(w.slab, 0, align_up(words * 8, 16), s));   // every tag = 0
   ResArgs a{};
   a.X = X; a.K = K; a.d = d; a.ldx = ldx; a.guess0 = guess0; a.out = out;
   a.maxiter = o->maxiter; a.tol = (float)o->tol; a.eps = (float)o->eps;
   a.mode = o->mode; a.has_noise = o->mode == GM_MODE_AIRCOMP && o->has_noise;
   a.P_max = o->P_max; a.noise_sd = std::sqrt(std::max(0.0, o->noise_var) / 2.0);
-  a.seed = o->seed; a.slab = w.slab; a.bar = bar; a.st = w.st;
-  (void)S;
+  a.seed = o->seed;
+  a.gran = reinterpret_cast<unsigned long long*>(w.slab);
+  a.bar = bar; a.st = w.st;
   hipEvent_t e0, e1;
   rc = record_pass_begin(c, s, &e0, &e1);
   if (rc) return rc;
-  HIPCHK(launch_resident(cfg, nch, a, s));
+  HIPCHK(launch_resident(cfg, cpb, nb, a, s));
   rc = record_pass_end(c, s, e0, e1);
   if (rc) return rc;
   KState* hst = reinterpret_cast<KState*>(c->host);
@@ -322,15 +326,16 @@ int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const
              bool split, bool guarded, bool* rejected) {
   *rejected = false;
   const int KT = gram_kt(K), KP = 32 * KT;
-  int nb_g;
-  if (split) {   // ~8K columns per block, whole rounds of one block per CU
-    nb_g = (int)std::max<int64_t>(1, (d + 8191) / 8192);
-    if (nb_g > c->num_cu) nb_g = (nb_g + c->num_cu - 1) / c->num_cu * c->num_cu;
-  } else {
-    nb_g = std::max(1, std::min(4 * c->num_cu, (int)((d + 4095) / 4096)));
-  }
-  const int64_t cpb = gram_cols_per_block(d, nb_g, split);
-  nb_g = (int)std::max<int64_t>(1, (d + cpb - 1) / cpb);
+  // split: the scaled f16 kernel (3 products), rerun as the bf16 split (4 products,
+  // the full fp32 exponent range) if its G came out non-finite (GMAGG_GRAM_KIND=bf16
+  // forces the bf16 kernel: A/B)
+  const char* kind_env = getenv("GMAGG_GRAM_KIND");
+  const bool force_bf16 = kind_env && strcmp(kind_env, "bf16") == 0;
+  GramKind kind = !split ? GramKind::F32 : force_bf16 ? GramKind::BF16 : GramKind::H16;
+  GramGrid gg = gram_grid(d, kind, c->num_cu);
+  const GramGrid gb = gram_grid(d, GramKind::BF16, c->num_cu);
+  const size_t slab_n = std::max(gram_slab_floats(KT, gg),
+                                 kind == GramKind::H16 ? gram_slab_floats(KT, gb) : 0);
   // closing pass: the STEP tile when it also yields the distances (guarded), else
   // the lighter sum-only tile
   const PassCfg ccfg = guarded ? cfg : light_cfg(K, cfg);
@@ -339,24 +344,28 @@ int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const
       1, std::min<int64_t>((d + J - 1) / J,
                            (int64_t)c->num_cu * pass_blocks_per_cu(ccfg, guarded ? 0 : 3)));
   Workspace w;
-  int rc = ensure_ws(c, K, d, nb_p, &w, gram_slab_floats(KT, nb_g), KP);
+  int rc = ensure_ws(c, K, d, nb_p, &w, slab_n, KP);
   if (rc) return rc;
   rc = ensure_host(c, sizeof(KState) + 4 * sizeof(double));
   if (rc) return rc;
   KState* hst = reinterpret_cast<KState*>(c->host);
   double* hsums = reinterpret_cast<double*>(c->host + sizeof(KState));
-  HIPCHK(hipMemsetAsync(w.st, 0, sizeof(KState), s));
   // centre p = guess0, staged to an aligned workspace copy (float4 loads)
   float* p = w.g[1];
   HIPCHK(hipMemcpyAsync(p, guess0, sizeof(float) * d, hipMemcpyDeviceToDevice, s));
+again:
+  HIPCHK(hipMemsetAsync(w.st, 0, sizeof(KState), s));
   hipEvent_t e0, e1;
   rc = record_pass_begin(c, s, &e0, &e1);
   if (rc) return rc;
-  HIPCHK(launch_gram(X, K, d, ldx, p, nb_g, w.gslab, w.G, s, split));
+  HIPCHK(launch_gram(X, K, d, ldx, p, kind, gg, w.gslab, w.G, w.st, s));
   rc = record_pass_end(c, s, e0, e1);
   if (rc) return rc;
   rc = allreduce(c, w.G, (int64_t)KP * KP, s);
   if (rc) return rc;
+  // a non-finite G (f16 overflow on any rank, or a non-finite input) sets
+  // gram_bad; checked after the all-reduce, so every rank takes the same branch
+  HIPCHK(launch_gram_check(w.G, KP, w.st, s));
   HIPCHK(launch_gram_solve(w.G, KP, K, o->maxiter, (float)o->tol, (float)o->eps, w.alpha, w.u,
                            w.coef, w.st, s));
   // closing pass: g = sum_k a_k x_k (+ the exact distances to g when guarded)
@@ -374,6 +383,11 @@ int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const
   HIPCHK(hipMemcpyAsync(hst, w.st, sizeof(KState), hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(hsums, w.sums + (S - 2), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (hst->gram_bad && kind == GramKind::H16) {   // rare: the f16 range was exceeded
+    kind = GramKind::BF16;
+    gg = gb;
+    goto again;
+  }
   if (guarded) {
     const double u = std::ldexp(1.0, -24);
     const double gn = std::sqrt(std::max(0.0, hsums[1]));
@@ -382,6 +396,11 @@ int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const
     const double pred = hst->guard_q / (1.0 - rho) / gn;
     const bool accurate = pred <= 1e-6;                     // NaN fails
     const bool floor_ok = !hst->converged || 2.0 * u * gn <= o->tol / 3.0;
+    static const bool dbg = getenv("GMAGG_GUARD_DEBUG") != nullptr;
+    if (dbg)
+      fprintf(stderr, "[gram guard] K=%lld d=%lld q=%.3e rho=%.3f |g|=%.4e pred=%.3e converged=%d "
+              "iters=%d floor_ok=%d accurate=%d\n", (long long)K, (long long)d, hst->guard_q, rho,
+              gn, pred, (int)hst->converged, (int)hst->iters, (int)floor_ok, (int)accurate);
     if (!accurate || !floor_ok) {
       *rejected = true;
       return GM_OK;
@@ -392,6 +411,7 @@ int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const
   r.last_movement = hst->last_movement;
   r.converged = hst->converged;
   r.algo_used = split ? GM_ALGO_GRAM : GM_ALGO_GRAM_F32;
+  r.gram_kind = kind == GramKind::H16 ? 1 : kind == GramKind::BF16 ? 2 : 3;
   r.guard = guarded ? GM_GUARD_ACCEPTED : GM_GUARD_NONE;
   if (res) *res = r;
   return GM_OK;
@@ -581,9 +601,10 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       c->d_total <= 0 && !c->comm && !c->ar_fn && pick_cfg(K, V, ldx, &cfg)) {
     const int J = cfg.LPR * cfg.V;
     const int64_t nch = (d + J - 1) / J;
-    if (nch <= resident_max_blocks(cfg, c->num_cu)) {
+    int cpb = 0, nbr = 0;
+    if (resident_plan(cfg, nch, c->num_cu, &cpb, &nbr)) {
       bool timed_out = false;
-      const int rc0 = run_resident(c, X, K, d, ldx, guess0, out, o, res, cfg, (int)nch, s,
+      const int rc0 = run_resident(c, X, K, d, ldx, guess0, out, o, res, cfg, cpb, nbr, s,
                                    &timed_out);
       if (rc0 || !timed_out) return rc0;
       // barrier timeout (e.g. a time-sliced GPU): the same problem, same draw keys,

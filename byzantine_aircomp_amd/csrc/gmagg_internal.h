@@ -20,7 +20,9 @@ struct alignas(64) KState {
   // Gram variant, written by gram_solve for the AUTO accuracy guard (api.hip):
   double guard_q;        // ||X'^T b||: one-step error of the K-space map (gram_verify)
   double guard_r;        // last / previous K-space movement (contraction estimate)
-  double pad[2];
+  int32_t gram_bad;      // the reduced Gram has a non-finite entry (f16 overflow or input)
+  int32_t pad0;
+  double pad1;
 };
 
 // Streaming pass configuration: V floats per lane per row, NW waves per
@@ -107,21 +109,33 @@ struct ResArgs {
   int mode, has_noise;
   double P_max, noise_sd;
   uint64_t seed;
-  double* slab;          // [2][gridDim.x][2K+2]
-  unsigned* bar;         // [0] arrivals, [1] generation, [2] timeout flag (zeroed per call)
+  unsigned long long* gran;  // [2][gridDim.x][2 (2K + 2 NW)] {tag, half} granules (zeroed per call)
+  unsigned* bar;         // [2] timeout flag (zeroed per call)
   KState* st;
 };
-int resident_max_blocks(const PassCfg& cfg, int num_cu);
-hipError_t launch_resident(const PassCfg& cfg, int grid, const ResArgs& a, hipStream_t s);
+// Plan a resident launch over nch chunks: chunks per block and blocks (false: the
+// grid cannot be co-resident / no kernel for the tile).
+bool resident_plan(const PassCfg& cfg, int64_t nch, int num_cu, int* cpb, int* nb);
+size_t resident_gran_words(int64_t K, const PassCfg& cfg, int nb);
+hipError_t launch_resident(const PassCfg& cfg, int cpb, int grid, const ResArgs& a, hipStream_t s);
 
 // Gram-space variant (gram.hip).  KT = K padded to 32-row tiles (0: unsupported).
-// split = true: bf16 h+m split on v_mfma_f32_32x32x16_bf16 (default);
-// false: exact f32-input v_mfma_f32_32x32x2_f32.
+// H16: scaled f16 h+m split, 3 products on v_mfma_f32_32x32x16_f16 (default);
+// BF16: bf16 h+m split, 4 products on v_mfma_f32_32x32x16_bf16 (fallback when
+// the f16 Gram is non-finite); F32: exact f32-input v_mfma_f32_32x32x2_f32.
+enum class GramKind { F32, BF16, H16 };
+struct GramGrid {
+  int nb;          // blocks
+  int64_t cpb;     // columns per block
+  int nseg;        // fp32 partials per block
+};
 int gram_kt(int64_t K);
-size_t gram_slab_floats(int KT, int nb);
-int64_t gram_cols_per_block(int64_t d, int nb, bool split);
-hipError_t launch_gram(const float* X, int64_t K, int64_t d, int64_t ldx, const float* p, int nb,
-                       float* slab, double* G, hipStream_t s, bool split);
+GramGrid gram_grid(int64_t d, GramKind kind, int num_cu);
+size_t gram_slab_floats(int KT, const GramGrid& g);
+hipError_t launch_gram(const float* X, int64_t K, int64_t d, int64_t ldx, const float* p,
+                       GramKind kind, const GramGrid& g, float* slab, double* G, KState* st,
+                       hipStream_t s);
+hipError_t launch_gram_check(const double* G, int KP, KState* st, hipStream_t s);
 hipError_t launch_gram_verify(const double* G, int KP, int64_t K, float eps, const double* u,
                               const double* alpha, const double* Dx, double* bvec, KState* st,
                               hipStream_t s);

@@ -369,6 +369,321 @@ __global__ void __launch_bounds__(512, 1) gram_split_partial(const float* __rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// Scaled fp16 split Gram (the default Gram path since round 2).
+//
+// Each centred element is scaled by a per-(row, block) power of two 2^e_k and
+// split as y = x' 2^e_k = h + m, h = f16(y), m = f16(y - h): h + m carries 22
+// significant bits (the remainder is <= 2^-22 |y|), and f16 x f16 products are
+// exact in fp32.  Three v_mfma_f32_32x32x16_f16 per 32x32 tile and 16 columns
+// (hh^T + hm^T + mh^T) then give the fp32 Gram of 22-bit inputs: the dropped
+// mm^T is <= 2^-22 |y_k||y_l| per column, a quarter of an fp32 rounding, where
+// the bf16 split (16 bits) needed all four products.  G_kl = 2^-(e_k+e_l) (the
+// accumulated tile), applied exactly (ldexp) when a partial is written.
+//
+// f16 has 5 exponent bits, hence the scale: e_k puts the row's largest |x'| over
+// the block's first two stages (128 columns, read before anything is
+// converted) at [2^3, 2^4).  Elements up to 4095x that size stay finite; much
+// smaller ones keep an absolute precision of 2^-24 (f16 subnormals, which the
+// f16 MFMA and conversion keep), i.e. 2^-27 of the row's largest element.  An
+// element beyond the headroom becomes inf, G non-finite: gram_check flags it
+// (KState::gram_bad) and the host reruns the bf16 split (api.hip run_gram).
+//
+// Block = 4 waves, ONE per SIMD with the whole 512-entry register file, and no
+// producer/consumer split: every wave streams a quarter of each 64-column stage
+// (16 rows x float4 per lane), converts it into the LDS h/m images and runs its
+// 9 tiles' MFMAs.  Three stages of loads are in flight in three register sets
+// (192 KiB per CU): while the MFMAs of stage s read LDS buffer s&1, each wave
+// commits stage s+1 (set (s+1)%3) into buffer (s+1)&1 four rows per 16-column
+// MFMA step and re-issues each committed row's registers for stage s+4 at once
+// (rolling).  One barrier per stage.  The bf16 kernel's two-role block held two
+// sets at most and its producers streamed 5.0 TB/s on their own
+// (profiles/r02_gram_split.txt).  Persistent: one block per CU over a contiguous
+// ~d/num_cu column range; the fp32 accumulators are flushed to a partial every
+// kH16Flush stages (8192 columns, the bf16 kernel's accumulation length).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kH16BK = 64;            // columns per stage
+constexpr int kH16LS = kH16BK + 8;    // LDS row stride (halves): 144 B
+constexpr int kH16Flush = 128;        // stages per fp32 partial
+
+template <int KT>
+using H16Lds = _Float16[2][2][GramShape<KT>::KP * kH16LS];   // [buffer][h|m][row][col]
+
+template <int KT, int NS>
+struct H16Stream {
+  static constexpr int RPT = GramShape<KT>::ROWS_PER_THREAD;
+  const float* X;
+  const float* p;
+  int64_t K, ldx, c_begin, c_end;
+  int r0, cg;
+  uint32_t voff;   // byte offset of this lane's row r0 within a row group (same for all groups)
+  f32x4 st[NS][RPT];
+  f32x4 pc[NS];
+  float cm[NS];    // 1 for a stage's real columns, 0 past c_end
+  float sc[RPT];   // 2^e_k for real rows, 0 for padding rows (>= K)
+
+  // Row group i (rows 16i + r0) is a raw buffer resource in SGPRs at row 16i plus
+  // the lane's VGPR offset r0 * ldx * 4 (the same for every full group).  Lanes
+  // past K read row 16i (or row 0 for a group wholly past K) and are zeroed by sc;
+  // columns past c_end re-read the stage's first columns, zeroed by cm.
+  __device__ __forceinline__ uint32_t stage_cols(int s, float& cmv) const {
+    const int64_t c0 = c_begin + (int64_t)s * kH16BK;
+    const bool cval = c0 + cg * 4 < c_end;
+    cmv = cval ? 1.f : 0.f;
+    return cval ? (uint32_t)(cg * 16) : 0u;
+  }
+  __device__ __forceinline__ f32x4 load_row(int s, int i, uint32_t lb) const {
+    const int64_t c0 = c_begin + (int64_t)s * kH16BK;
+    const int64_t rem = K - 16 * i;                        // wave-uniform
+    const int64_t rb = rem > 0 ? 16 * i : 0;
+    const uint32_t off = (rem >= 16 || r0 < rem) ? voff + lb : lb;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(X + c0 + rb * ldx), 0, -1, 0x00020000);
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2));
+  }
+  __device__ __forceinline__ f32x4 load_p(int s, float cmv) const {
+    const int64_t c0 = c_begin + (int64_t)s * kH16BK;
+    return *reinterpret_cast<const f32x4*>(p + c0 + (cmv != 0.f ? cg * 4 : 0));
+  }
+  template <int SET>
+  __device__ __forceinline__ void fetch(int s) {
+    const uint32_t lb = stage_cols(s, cm[SET]);
+    pc[SET] = load_p(s, cm[SET]);
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) st[SET][i] = load_row(s, i, lb);
+  }
+  template <int SET>
+  __device__ __forceinline__ float absmax(int i) const {
+    const f32x4 x = (st[SET][i] - pc[SET]) * cm[SET];
+    return fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
+  }
+  template <int SET>
+  __device__ __forceinline__ void commit_row(int i, _Float16* Lh, _Float16* Lm) {
+    const int r = r0 + 16 * i;
+    const f32x4 x = (st[SET][i] - pc[SET]) * (sc[i] * cm[SET]);
+    const f32x2 x01 = {x[0], x[1]}, x23 = {x[2], x[3]};
+    const f16x2 h01 = __builtin_convertvector(x01, f16x2);
+    const f16x2 h23 = __builtin_convertvector(x23, f16x2);
+    const f16x2 m01 = __builtin_convertvector(x01 - __builtin_convertvector(h01, f32x2), f16x2);
+    const f16x2 m23 = __builtin_convertvector(x23 - __builtin_convertvector(h23, f32x2), f16x2);
+    *reinterpret_cast<f16x4*>(Lh + r * kH16LS + cg * 4) = f16x4{h01[0], h01[1], h23[0], h23[1]};
+    *reinterpret_cast<f16x4*>(Lm + r * kH16LS + cg * 4) = f16x4{m01[0], m01[1], m23[0], m23[1]};
+  }
+  // commit stage data of set SET into (Lh, Lm), re-issuing each row's registers
+  // for stage sn right after its commit (rolling)
+  template <int SET>
+  __device__ __forceinline__ void commit_refetch(_Float16* Lh, _Float16* Lm, int sn) {
+    float cmn;
+    const uint32_t lbn = stage_cols(sn, cmn);
+    const f32x4 pcn = load_p(sn, cmn);
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      commit_row<SET>(i, Lh, Lm);
+      asm volatile("" ::: "memory");       // the re-issue stays behind this row's commit
+      st[SET][i] = load_row(sn, i, lbn);
+    }
+    pc[SET] = pcn;
+    cm[SET] = cmn;
+  }
+};
+
+// Wave W's tiles for one 16-column step, ordered by column tile b descending so
+// a b fragment is read just before the MFMAs that use it and dies after them:
+// b = KT-1 .. KT-1-W carry two tiles, (W, b) and (KT-1-W, b); b = KT-2-W .. W one,
+// (W, b).  Live fragments: the two row tiles' h/m + the current b's (+ the next
+// b's, prefetched by the scheduler), instead of every b of the step.
+// acc slot of tile (a, b) = its position in wave_tile's order.
+template <int KT, int W>
+struct H16Order {
+  static constexpr int first = KT - W;        // tiles (W, W..KT-1) come first in wave_tile
+  static constexpr int slot_w(int b) { return b - W; }
+  static constexpr int slot_o(int b) { return first + (b - (KT - 1 - W)); }
+};
+
+template <int KT, int W, int B>
+__device__ __forceinline__ void h16_step_b(const _Float16* Lh, const _Float16* Lm, int off,
+                                           const f16x8& haw, const f16x8& maw,
+                                           const f16x8& hao, const f16x8& mao,
+                                           f32x16 (&acc)[GramShape<KT>::PER_WAVE]) {
+  if constexpr (B >= W) {
+    using O = H16Order<KT, W>;
+    const f16x8 hb = *reinterpret_cast<const f16x8*>(Lh + B * 32 * kH16LS + off);
+    const f16x8 mb = *reinterpret_cast<const f16x8*>(Lm + B * 32 * kH16LS + off);
+    constexpr int tw = O::slot_w(B);
+    acc[tw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(haw, hb, acc[tw], 0, 0, 0);
+    acc[tw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(haw, mb, acc[tw], 0, 0, 0);
+    acc[tw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(maw, hb, acc[tw], 0, 0, 0);
+    if constexpr (KT > 1 && B >= KT - 1 - W) {
+      constexpr int to = O::slot_o(B);
+      acc[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(hao, hb, acc[to], 0, 0, 0);
+      acc[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(hao, mb, acc[to], 0, 0, 0);
+      acc[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(mao, hb, acc[to], 0, 0, 0);
+    }
+    h16_step_b<KT, W, B - 1>(Lh, Lm, off, haw, maw, hao, mao, acc);
+  }
+}
+
+template <int KT, int W>
+__device__ __forceinline__ void h16_step(const _Float16* Lh, const _Float16* Lm, int off,
+                                         f32x16 (&acc)[GramShape<KT>::PER_WAVE]) {
+  constexpr int AO = KT == 1 ? 0 : KT - 1 - W;
+  const f16x8 haw = *reinterpret_cast<const f16x8*>(Lh + W * 32 * kH16LS + off);
+  const f16x8 maw = *reinterpret_cast<const f16x8*>(Lm + W * 32 * kH16LS + off);
+  const f16x8 hao = *reinterpret_cast<const f16x8*>(Lh + AO * 32 * kH16LS + off);
+  const f16x8 mao = *reinterpret_cast<const f16x8*>(Lm + AO * 32 * kH16LS + off);
+  h16_step_b<KT, W, KT - 1>(Lh, Lm, off, haw, maw, hao, mao, acc);
+}
+
+// Producer waves (4..7): stream every stage into the LDS images, two stages of
+// loads in flight (rolling re-issue).  Three sets fit the 256 VGPRs of a
+// two-waves-per-SIMD block only without the unroll by 6 that static set indices
+// need (the compiler spilled 50-300 VGPRs at every unroll >= 3 tried).
+constexpr int kH16Sets = 2;
+
+template <int KT, int DBG>
+__device__ __forceinline__ void h16_producer(const float* __restrict__ X, int64_t K, int64_t ldx,
+                                             const float* __restrict__ p, int64_t c_begin,
+                                             int64_t c_end, int nstage, H16Lds<KT>& lds,
+                                             int* s_exp) {
+  constexpr int RPT = GramShape<KT>::ROWS_PER_THREAD;
+  H16Stream<KT, kH16Sets> P;
+  const int t = threadIdx.x - 256;
+  P.X = X; P.p = p; P.K = K; P.ldx = ldx; P.c_begin = c_begin; P.c_end = c_end;
+  P.r0 = t >> 4; P.cg = t & 15;
+  P.voff = (uint32_t)P.r0 * (uint32_t)ldx * 4u;
+  if (nstage == 0 || DBG == 2) {                 // no columns: meet the consumers' barriers
+    for (int s = 0; s <= (DBG == 2 ? nstage : 0); ++s) __syncthreads();   // DBG 2: no loads
+    return;
+  }
+  // Every fetch and commit is unconditional: a stage index past the end is
+  // clamped to the last stage (a re-read of <= 3 stages per block) and a commit
+  // past the end fills the LDS buffer nobody reads.  A conditional re-issue would
+  // keep the set's old value live on the skipped path (a fourth set: spills).
+  const int last = nstage - 1;
+  P.template fetch<0>(0);
+  P.template fetch<1>(min(1, last));
+  // per-row scale from the first two stages: the 16 lanes of a row group hold its
+  // 64 columns (lanes 16j .. 16j+15 share r0)
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    float mx = fmaxf(P.template absmax<0>(i), P.template absmax<1>(i));
+    mx = fmaxf(mx, __shfl_xor(mx, 1, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 2, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 4, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 8, 16));
+    int ex = 0;
+    (void)frexpf(mx, &ex);                       // mx = f 2^ex, f in [0.5, 1)
+    int e = (mx > 0.f && mx <= 3.0e38f) ? 4 - ex : 0;
+    e = e < -100 ? -100 : (e > 100 ? 100 : e);
+    const bool real = P.r0 + 16 * i < K;
+    P.sc[i] = real ? ldexpf(1.f, e) : 0.f;
+    if (P.cg == 0) s_exp[P.r0 + 16 * i] = real ? e : 0;
+  }
+  P.template commit_refetch<0>(lds[0][0], lds[0][1], min(2, last));
+  __syncthreads();                               // stage 0 in buffer 0, exponents published
+  // while the consumers run stage s: commit s+1 (set and buffer (s+1)&1),
+  // re-issuing its rows for s+3 one by one: stages s+2 and s+3 in flight.
+  // Unrolled by 2 so set and buffer indices are compile-time.
+#define GMK_H16_STEP(J)                                                                     \
+  {                                                                                         \
+    if (s + J >= nstage) break;                                                             \
+    P.template commit_refetch<(J + 1) & 1>(lds[(J + 1) & 1][0], lds[(J + 1) & 1][1],        \
+                                           min(s + J + 3, last));                           \
+    __syncthreads();                                                                        \
+  }
+  for (int s = 0; s < nstage; s += 2) {
+    GMK_H16_STEP(0) GMK_H16_STEP(1)
+  }
+#undef GMK_H16_STEP
+}
+
+// Consumer wave W (0..3; W < 0: no tiles for K <= 128): MFMAs of every stage,
+// fp32 partial `seg` to slab[(blockIdx.x * nseg + seg)][tiles][1024], unscaled.
+template <int KT, int W, int DBG>
+__device__ __forceinline__ void h16_consumer(int nstage, int nseg, float* __restrict__ slab,
+                                             H16Lds<KT>& lds, const int* s_exp) {
+  using Sh = GramShape<KT>;
+  constexpr int NT = Sh::PER_WAVE;
+  constexpr bool MMA = W >= 0 && DBG != 1;     // DBG 1: timing probe without MFMAs
+  constexpr int WW = W < 0 ? 0 : W;
+  const int lane = threadIdx.x & 63;
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+  float* base = slab + (int64_t)blockIdx.x * nseg * Sh::TILES * 1024;
+  auto flush = [&](int seg, bool zero) {
+    float* out = base + (int64_t)seg * Sh::TILES * 1024;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      int a, b;
+      wave_tile<KT>(WW, t, a, b);
+      float* o = out + tri_index(a, b, KT) * 1024;
+      const int ec = s_exp[b * 32 + (lane & 31)];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int er = s_exp[a * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)];
+        o[e * 64 + lane] = zero ? 0.f : ldexpf(acc[t][e], -(er + ec));
+        acc[t][e] = 0.f;
+      }
+    }
+  };
+  const int fo = (lane & 31) * kH16LS + (lane >> 5) * 8;   // fragment offset in a tile
+  __syncthreads();                                           // stage 0 is in buffer 0
+  int seg = 0;
+  for (int s = 0; s < nstage; ++s) {
+    if constexpr (MMA) {
+      const _Float16* Lh = lds[s & 1][0];
+      const _Float16* Lm = lds[s & 1][1];
+#pragma unroll
+      for (int ks = 0; ks < kH16BK / 16; ++ks) h16_step<KT, WW>(Lh, Lm, ks * 16 + fo, acc);
+      if ((s + 1) % kH16Flush == 0 || s + 1 == nstage) flush(seg++, false);
+    }
+    __syncthreads();
+  }
+  if constexpr (MMA)
+    for (; seg < nseg; ++seg) flush(seg, true);              // blocks with fewer stages
+}
+
+template <int KT, int DBG = 0>
+__global__ void __launch_bounds__(512, 1) gram_h16_partial(const float* __restrict__ X, int64_t K,
+                                                           int64_t d, int64_t ldx,
+                                                           const float* __restrict__ p,
+                                                           int64_t cols_per_block, int nseg,
+                                                           float* __restrict__ slab) {
+  __shared__ H16Lds<KT> lds;
+  __shared__ int s_exp[GramShape<KT>::KP];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t c_begin = (int64_t)blockIdx.x * cols_per_block;
+  const int64_t c_end = c_begin + cols_per_block < d ? c_begin + cols_per_block : d;
+  const int nstage = c_begin < c_end ? (int)((c_end - c_begin + kH16BK - 1) / kH16BK) : 0;
+  if (w >= 4) {
+    h16_producer<KT, DBG>(X, K, ldx, p, c_begin, c_end, nstage, lds, s_exp);
+    return;
+  }
+  if constexpr (KT == 8) {
+    switch (w) {
+      case 0: h16_consumer<KT, 0, DBG>(nstage, nseg, slab, lds, s_exp); break;
+      case 1: h16_consumer<KT, 1, DBG>(nstage, nseg, slab, lds, s_exp); break;
+      case 2: h16_consumer<KT, 2, DBG>(nstage, nseg, slab, lds, s_exp); break;
+      default: h16_consumer<KT, 3, DBG>(nstage, nseg, slab, lds, s_exp); break;
+    }
+  } else if constexpr (KT == 4) {
+    switch (w) {
+      case 0: h16_consumer<KT, 0, DBG>(nstage, nseg, slab, lds, s_exp); break;
+      case 1: h16_consumer<KT, 1, DBG>(nstage, nseg, slab, lds, s_exp); break;
+      default: h16_consumer<KT, -1, DBG>(nstage, nseg, slab, lds, s_exp); break;
+    }
+  } else {
+    if (w == 0) h16_consumer<KT, 0, DBG>(nstage, nseg, slab, lds, s_exp);
+    else h16_consumer<KT, -1, DBG>(nstage, nseg, slab, lds, s_exp);
+  }
+}
+
 // Sum the fp32 block partials in fp64 in a fixed order, in two steps so that
 // every element has many loads in flight: gram_reduce_part sums blocks
 // y, y+NG, y+2NG, ... (four interleaved fp64 chains, combined in order) into
@@ -393,14 +708,17 @@ __global__ void __launch_bounds__(256) gram_reduce_part(const float* __restrict_
 }
 
 __global__ void __launch_bounds__(256) gram_reduce_final(const double* __restrict__ tmp, int NG,
-                                                         int KT, double* __restrict__ G) {
+                                                         int KT, double* __restrict__ G,
+                                                         KState* st) {
   const int tiles = KT * (KT + 1) / 2;
   const int64_t n = (int64_t)tiles * 1024;
   const int KP = 32 * KT;
+  bool bad = false;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     double s = 0.0;
     for (int y = 0; y < NG; ++y) s += tmp[(int64_t)y * n + e];
+    bad |= !isfinite(s);
     const int tix = (int)(e >> 10), el = (int)(e & 1023);
     int a = 0;
     while (tri_index(a, KT - 1, KT) < tix) ++a;        // row tile of this triangle index
@@ -411,6 +729,7 @@ __global__ void __launch_bounds__(256) gram_reduce_final(const double* __restric
     G[(int64_t)row * KP + col] = s;
     G[(int64_t)col * KP + row] = s;
   }
+  if (bad) st->gram_bad = 1;                           // plain vector store, same value
 }
 
 // The Weiszfeld loop in K-space, fp64, all iterations in one launch.  Writes
@@ -520,6 +839,18 @@ __global__ void __launch_bounds__(1024) gram_verify(const double* __restrict__ G
   if (tid == 0) st->guard_q = sqrt(q > 0.0 ? q : (q != q ? q : 0.0));
 }
 
+// Non-finite entries in the (all-reduced) Gram -> st->gram_bad.  One block.
+__global__ void __launch_bounds__(1024) gram_check(const double* __restrict__ G, int KP, KState* st) {
+  bool bad = false;
+  for (int i = threadIdx.x; i < KP * KP; i += blockDim.x) bad |= !isfinite(G[i]);
+  if (bad) st->gram_bad = 1;                           // plain vector store, same value
+}
+
+hipError_t launch_gram_check(const double* G, int KP, KState* st, hipStream_t s) {
+  hipLaunchKernelGGL(gram_check, dim3(1), dim3(1024), 0, s, G, KP, st);
+  return hipGetLastError();
+}
+
 hipError_t launch_gram_verify(const double* G, int KP, int64_t K, float eps, const double* u,
                               const double* alpha, const double* Dx, double* bvec, KState* st,
                               hipStream_t s) {
@@ -536,9 +867,9 @@ static hipError_t launch_gram_kt(const float* X, int64_t K, int64_t d, int64_t l
 
 int gram_kt(int64_t K) { return K <= 32 ? 1 : K <= 64 ? 2 : K <= 128 ? 4 : K <= 256 ? 8 : 0; }
 
-// block partials [nb][tiles][1024] fp32, then the reduction's fp64 tmp[kReduceGroups][n]
-size_t gram_slab_floats(int KT, int nb) {
-  return (size_t)(nb + 2 * kReduceGroups) * (KT * (KT + 1) / 2) * 1024;
+// partials [nb * nseg][tiles][1024] fp32, then the reduction's fp64 tmp[kReduceGroups][n]
+size_t gram_slab_floats(int KT, const GramGrid& g) {
+  return (size_t)(g.nb * g.nseg + 2 * kReduceGroups) * (KT * (KT + 1) / 2) * 1024;
 }
 
 template <int KT>
@@ -559,35 +890,85 @@ static hipError_t launch_split_kt(const float* X, int64_t K, int64_t d, int64_t 
   return hipGetLastError();
 }
 
-int64_t gram_cols_per_block(int64_t d, int nb, bool split) {
-  const int64_t q = split ? kSplitBK : kGramJC;
-  return ((d + nb - 1) / nb + q - 1) / q * q;
+template <int KT>
+static hipError_t launch_h16_kt(const float* X, int64_t K, int64_t d, int64_t ldx, const float* p,
+                                int nb, int64_t cpb, int nseg, float* slab, hipStream_t s) {
+  // GMAGG_GRAM_DEBUG = 1 / 2: timing probes without MFMAs / without loads (wrong G)
+  static const int dbg = [] { const char* e = getenv("GMAGG_GRAM_DEBUG"); return e ? atoi(e) : 0; }();
+  if (dbg == 1)
+    hipLaunchKernelGGL((gram_h16_partial<KT, 1>), dim3(nb), dim3(512), 0, s, X, K, d, ldx, p, cpb,
+                       nseg, slab);
+  else if (dbg == 2)
+    hipLaunchKernelGGL((gram_h16_partial<KT, 2>), dim3(nb), dim3(512), 0, s, X, K, d, ldx, p, cpb,
+                       nseg, slab);
+  else
+    hipLaunchKernelGGL((gram_h16_partial<KT, 0>), dim3(nb), dim3(512), 0, s, X, K, d, ldx, p, cpb,
+                       nseg, slab);
+  return hipGetLastError();
 }
 
-hipError_t launch_gram(const float* X, int64_t K, int64_t d, int64_t ldx, const float* p, int nb,
-                       float* slab, double* G, hipStream_t s, bool split) {
+// Grid of one Gram launch: blocks, columns per block, fp32 partials per block.
+GramGrid gram_grid(int64_t d, GramKind kind, int num_cu) {
+  GramGrid g{};
+  if (kind == GramKind::H16) {          // persistent: one block per CU
+    g.nb = (int)std::max<int64_t>(1, std::min<int64_t>(num_cu, (d + kH16BK - 1) / kH16BK));
+    g.cpb = ((d + g.nb - 1) / g.nb + kH16BK - 1) / kH16BK * kH16BK;
+    g.nb = (int)std::max<int64_t>(1, (d + g.cpb - 1) / g.cpb);
+    const int64_t st = g.cpb / kH16BK;
+    g.nseg = (int)((st + kH16Flush - 1) / kH16Flush);
+    return g;
+  }
+  const bool split = kind == GramKind::BF16;
+  if (split) {   // ~8K columns per block, whole rounds of one block per CU
+    g.nb = (int)std::max<int64_t>(1, (d + 8191) / 8192);
+    if (g.nb > num_cu) g.nb = (g.nb + num_cu - 1) / num_cu * num_cu;
+  } else {
+    g.nb = std::max(1, std::min(4 * num_cu, (int)((d + 4095) / 4096)));
+  }
+  const int64_t q = split ? kSplitBK : kGramJC;
+  g.cpb = ((d + g.nb - 1) / g.nb + q - 1) / q * q;
+  g.nb = (int)std::max<int64_t>(1, (d + g.cpb - 1) / g.cpb);
+  g.nseg = 1;
+  return g;
+}
+
+hipError_t launch_gram(const float* X, int64_t K, int64_t d, int64_t ldx, const float* p,
+                       GramKind kind, const GramGrid& g, float* slab, double* G, KState* st,
+                       hipStream_t s) {
   const int KT = gram_kt(K);
-  const int64_t cpb = gram_cols_per_block(d, nb, split);
+  const int nb = g.nb;
+  const int64_t cpb = g.cpb;
   hipError_t e;
-  switch (KT * (split ? -1 : 1)) {
-    case 1: e = launch_gram_kt<1>(X, K, d, ldx, p, nb, cpb, slab, s); break;
-    case 2: e = launch_gram_kt<2>(X, K, d, ldx, p, nb, cpb, slab, s); break;
-    case 4: e = launch_gram_kt<4>(X, K, d, ldx, p, nb, cpb, slab, s); break;
-    case 8: e = launch_gram_kt<8>(X, K, d, ldx, p, nb, cpb, slab, s); break;
-    case -1: e = launch_split_kt<1>(X, K, d, ldx, p, nb, cpb, slab, s); break;
-    case -2: e = launch_split_kt<2>(X, K, d, ldx, p, nb, cpb, slab, s); break;
-    case -4: e = launch_split_kt<4>(X, K, d, ldx, p, nb, cpb, slab, s); break;
-    case -8: e = launch_split_kt<8>(X, K, d, ldx, p, nb, cpb, slab, s); break;
-    default: return hipErrorInvalidValue;
+  if (kind == GramKind::H16) {
+    switch (KT) {
+      case 1: e = launch_h16_kt<1>(X, K, d, ldx, p, nb, cpb, g.nseg, slab, s); break;
+      case 2: e = launch_h16_kt<2>(X, K, d, ldx, p, nb, cpb, g.nseg, slab, s); break;
+      case 4: e = launch_h16_kt<4>(X, K, d, ldx, p, nb, cpb, g.nseg, slab, s); break;
+      case 8: e = launch_h16_kt<8>(X, K, d, ldx, p, nb, cpb, g.nseg, slab, s); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (KT * (kind == GramKind::BF16 ? -1 : 1)) {
+      case 1: e = launch_gram_kt<1>(X, K, d, ldx, p, nb, cpb, slab, s); break;
+      case 2: e = launch_gram_kt<2>(X, K, d, ldx, p, nb, cpb, slab, s); break;
+      case 4: e = launch_gram_kt<4>(X, K, d, ldx, p, nb, cpb, slab, s); break;
+      case 8: e = launch_gram_kt<8>(X, K, d, ldx, p, nb, cpb, slab, s); break;
+      case -1: e = launch_split_kt<1>(X, K, d, ldx, p, nb, cpb, slab, s); break;
+      case -2: e = launch_split_kt<2>(X, K, d, ldx, p, nb, cpb, slab, s); break;
+      case -4: e = launch_split_kt<4>(X, K, d, ldx, p, nb, cpb, slab, s); break;
+      case -8: e = launch_split_kt<8>(X, K, d, ldx, p, nb, cpb, slab, s); break;
+      default: return hipErrorInvalidValue;
+    }
   }
   if (e != hipSuccess) return e;
+  const int parts = nb * g.nseg;
   const int64_t n = (int64_t)(KT * (KT + 1) / 2) * 1024;
-  const int ng = std::min(kReduceGroups, nb);
-  double* tmp = reinterpret_cast<double*>(slab + (size_t)nb * n);
+  const int ng = std::min(kReduceGroups, parts);
+  double* tmp = reinterpret_cast<double*>(slab + (size_t)parts * n);
   hipLaunchKernelGGL(gram_reduce_part, dim3((unsigned)((n + 255) / 256), ng), dim3(256), 0, s,
-                     slab, nb, n, tmp);
+                     slab, parts, n, tmp);
   hipLaunchKernelGGL(gram_reduce_final, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tmp,
-                     ng, KT, G);
+                     ng, KT, G, st);
   return hipGetLastError();
 }
 

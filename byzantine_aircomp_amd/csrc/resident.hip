@@ -4,14 +4,26 @@
 //
 // At that size a launch-per-phase loop is launch-bound (3 kernels + polls per
 // iteration).  Here ONE cooperative launch runs every iteration: each block
-// owns one J-column chunk of X, loaded into VGPRs once; per iteration it
-//   1. reads every block's partials of the previous pass from a double-buffered
-//      slab and reduces them in a fixed order (every block computes the
-//      identical K-space step redundantly: no second barrier, no broadcast),
+// owns CPB consecutive J-column chunks of X, loaded into VGPRs once; per
+// iteration it
+//   1. gathers every block's partials of the previous pass and reduces them in
+//      a fixed order (every block computes the identical K-space step
+//      redundantly: no broadcast),
 //   2. takes the tol test (M:182) and forms the next coefficients (M:178-179,
-//      or the OMA2 fold for gm, M:146-155 / M:401-412, Philox draws),
-//   3. runs phases A/B of the streaming pass on its register tile,
-//   4. publishes its partials and meets the others at ONE grid barrier.
+//      or the OMA2 fold for gm, M:146-155 / M:401-412, Philox draws) — one
+//      wave, lane = client, when K <= 64,
+//   3. runs phases A/B of the streaming pass on its register tiles,
+//   4. publishes its partials.
+// The exchange is the data itself: every partial is an fp64 value carried by two
+// 8-byte {tag, 32-bit half} granules, each written by ONE agent-scope relaxed
+// (write-through) store; readers poll the granules with agent-scope relaxed loads
+// until every tag equals the pass (cdna_hip_programming.md Guideline 16, R2).  No
+// grid barrier, no release/acquire fences: the r1 version (62 one-chunk blocks,
+// counter barrier + fenced slab) spent 5.05 us of a 12.4 us iteration in the
+// barrier and 2.15 us in the slab reduction.  Passes alternate
+// between two granule buffers: a block writes pass p+2 into p's buffer only after
+// it has read every block's pass p+1, which each block published after reading
+// pass p, so no pass is overwritten before every block has read it.
 // The iterate never leaves the chip until the final write.  Draw keys are the
 // same as the launch-per-phase path's, so both give the same gm results.
 #include "device_util.h"
@@ -19,7 +31,7 @@
 #include "philox.h"
 
 #ifndef GMK_RES_SLEEP
-#define GMK_RES_SLEEP 1   // spin back-off of the grid barrier (A/B knob)
+#define GMK_RES_SLEEP 1   // spin back-off of the granule polls (A/B knob)
 #endif
 
 // -DGMK_RES_PROF: block 0 / thread 0 accumulates s_memrealtime (100 MHz) deltas per
@@ -39,52 +51,69 @@ namespace gmk {
 
 // (ResArgs: gmagg_internal.h)
 
-constexpr uint64_t kBarrierTicks = 200000000ull;   // 2 s at the 100 MHz real-time clock
+constexpr uint64_t kPollTicks = 200000000ull;   // 2 s at the 100 MHz real-time clock
 
-// Grid barrier: arrival counter + generation word, agent-scope release before
-// arriving and acquire after leaving (cdna_hip_programming.md §6 G16).  The spin
-// is bounded in WALL time (s_memrealtime, 100 MHz: kBarrierTicks = 2 s, so a
-// time-sliced GPU does not trip it by spinning slowly): on timeout a flag is
-// raised, every block gives up, and the host reruns the problem on the
-// streaming path (api.hip run_resident).
-__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned nblocks, unsigned& gen,
-                                          int* s_ok) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int ok = 1;
-    const unsigned g = gen;
-    if (__hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-        nblocks - 1) {
-      __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&bar[1], g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      unsigned spins = 0;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
-#if GMK_RES_SLEEP > 0
-        __builtin_amdgcn_s_sleep(GMK_RES_SLEEP);
-#endif
-        if (((++spins & 1023u) == 0 &&
-             __builtin_amdgcn_s_memrealtime() - t0 > kBarrierTicks) ||
-            __hip_atomic_load(&bar[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-          __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok = 0;
-          break;
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    gen = g + 1;
-    *s_ok = ok;
-  }
-  __syncthreads();
-  return *s_ok != 0;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__device__ __forceinline__ void put_value(gu64* g, unsigned tag, double v) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned long long t = (unsigned long long)tag << 32;
+  __hip_atomic_store(g, t | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(g + 1, t | (u & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int V, int NW, int LPR, int R>
+// Sum over blocks b = 0..nb-1 (in that order) of value `col` of pass `tag`:
+// every granule pair is loaded at once (NB_CHUNK blocks per round trip), re-read
+// until all tags match.  The poll is bounded in WALL time (s_memrealtime): on
+// timeout (a time-sliced GPU, blocks not co-resident) the flag tmo is raised and
+// every block gives up; the host then reruns the problem on the streaming path.
+constexpr int kNbChunk = 8;
+
+__device__ __forceinline__ bool gather_value(const gu64* g, int64_t bstride, unsigned nb,
+                                             unsigned tag, gu32* tmo, double& sum) {
+  sum = 0.0;
+  for (unsigned b0 = 0; b0 < nb; b0 += kNbChunk) {
+    const int n = (int)(nb - b0 < (unsigned)kNbChunk ? nb - b0 : kNbChunk);
+    unsigned long long hi[kNbChunk], lo[kNbChunk];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j < kNbChunk; ++j) {
+        if (j < n) {
+          const gu64* q = g + (int64_t)(b0 + j) * bstride;
+          hi[j] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          lo[j] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok &= (unsigned)(hi[j] >> 32) == tag && (unsigned)(lo[j] >> 32) == tag;
+        }
+      }
+      if (ok) break;
+#if GMK_RES_SLEEP > 0
+      __builtin_amdgcn_s_sleep(GMK_RES_SLEEP);
+#endif
+      if (((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t0 > kPollTicks) ||
+          __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kNbChunk; ++j)
+      if (j < n)
+        sum += __longlong_as_double((long long)(((hi[j] & 0xffffffffull) << 32) |
+                                                (lo[j] & 0xffffffffull)));
+  }
+  return true;
+}
+
+// Granule slots of one block and pass: value v at [2v, 2v+1];
+//   v < K: D2_k; K <= v < 2K: ||x_k||^2 (INIT); 2K + 2w, 2K + 2w + 1: wave w's
+//   movement and ||g||^2 partials.
+template <int NW>
+__host__ __device__ constexpr int64_t res_values(int64_t K) { return 2 * K + 2 * NW; }
+
+template <int V, int NW, int LPR, int R, int CPB>
 __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   constexpr int QW = 64 / LPR;
   constexpr int NRG = NW * QW;
@@ -92,15 +121,16 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   constexpr int RPL = R > LPR ? R / LPR : 1;
   constexpr int SPAN = R < LPR ? LPR / R : 1;
   constexpr int KMAX = NRG * R;
+  constexpr int JB = J * CPB;                       // columns per block
+  static_assert(JB <= NW * 64, "one finisher column per thread");
 
-  __shared__ float s_red[NW][J];
-  __shared__ float s_g[J];
+  __shared__ float s_red[NW][JB];
+  __shared__ float s_g[JB];
   __shared__ float s_coef[KMAX];
   __shared__ double s_d2[KMAX];
   __shared__ double s_r[KMAX];
-  __shared__ double s_fin[2][NW];
   __shared__ double s_tot[2];
-  __shared__ double s_part[NW * 64];
+  __shared__ double s_wp[2 * NW];
   __shared__ double scratch[16];
   __shared__ float s_anoise;
   __shared__ int s_ok;
@@ -111,84 +141,87 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   const int rg = w * QW + q;
   const int64_t K = a.K, d = a.d;
   const unsigned nb = gridDim.x;
-  const int64_t S = 2 * K + 2;
-  const int64_t ch = blockIdx.x;
-  const int64_t col = ch * J + (int64_t)c * V;
-  const bool cval = col < d;
-  const int64_t gj = ch * J + tid;
-  const bool fin = tid < J && gj < d;
-  unsigned gen = 0;
+  const int64_t NV = res_values<NW>(K);            // values per block and pass
+  const int64_t ch0 = (int64_t)blockIdx.x * CPB;   // first chunk of this block
+  const int64_t gj = ch0 * J + tid;                // finisher column (tid < JB)
+  const bool fin = tid < JB && gj < d;
+  gu64* gran = (gu64*)a.gran;                      // [2][nb][2 NV]
+  gu32* tmo = (gu32*)a.bar + 2;
+  if (tid == 0) s_ok = 1;
 
-  // ---- the block's tile: loaded once, resident for the whole call
-  float x[R][V];
+  // ---- the block's tiles: loaded once, resident for the whole call
+  float x[CPB][R][V];
 #pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const int64_t k = rg + (int64_t)NRG * i;
+  for (int h = 0; h < CPB; ++h) {
+    const int64_t col = (ch0 + h) * J + (int64_t)c * V;
+    const bool cval = col < d;
 #pragma unroll
-    for (int v = 0; v < V; ++v) x[i][v] = (cval && k < K) ? a.X[k * a.ldx + col + v] : 0.f;
+    for (int i = 0; i < R; ++i) {
+      const int64_t k = rg + (int64_t)NRG * i;
+#pragma unroll
+      for (int v = 0; v < V; ++v) x[h][i][v] = (cval && k < K) ? a.X[k * a.ldx + col + v] : 0.f;
+    }
   }
   float gcur = fin ? a.guess0[gj] : 0.f;       // finisher thread: the iterate at column gj
 
   const int i_c = row_of_lane<LPR, R>(c);
-  auto publish = [&](int buf, const double* racc, const double* racc2, double mv, double gn) {
-    double* out = a.slab + ((int64_t)buf * nb + blockIdx.x) * S;
+  // publish this block's partials of pass p (granules, tag p + 1, buffer p & 1)
+  auto publish = [&](int64_t p, const double* racc, const double* racc2, double mv, double gn) {
+    gu64* out = gran + ((p & 1) * nb + blockIdx.x) * 2 * NV;
+    const unsigned tag = (unsigned)(p + 1);
     if ((c % SPAN) == 0) {
 #pragma unroll
       for (int m = 0; m < RPL; ++m) {
         const int64_t k = rg + (int64_t)NRG * (i_c + m);
         if (k < K) {
-          out[k] = racc[m];
-          if (racc2) out[K + k] = racc2[m];
+          put_value(out + 2 * k, tag, racc[m]);
+          if (racc2) put_value(out + 2 * (K + k), tag, racc2[m]);
         }
       }
     }
     mv = wave_sum(mv);
     gn = wave_sum(gn);
     if (lane == 0) {
-      s_fin[0][w] = mv;
-      s_fin[1][w] = gn;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      double m = 0.0, g = 0.0;
-      for (int ww = 0; ww < NW; ++ww) {
-        m += s_fin[0][ww];
-        g += s_fin[1][ww];
-      }
-      out[2 * K] = m;
-      out[2 * K + 1] = g;
+      put_value(out + 2 * (2 * K + 2 * w), tag, mv);
+      put_value(out + 2 * (2 * K + 2 * w + 1), tag, gn);
     }
   };
 
-  // ---- INIT: distances to g_0, ||x_k||^2 and ||g_0||^2 -> slab buffer 0
+  // ---- INIT: distances to g_0, ||x_k||^2 and ||g_0||^2 (pass 0)
   {
-    float gv[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) gv[v] = cval ? a.guess0[col + v] : 0.f;
-    float e[R], e2[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const float t = x[i][v] - gv[v];
-        s1 = fmaf(t, t, s1);
-        s2 = fmaf(x[i][v], x[i][v], s2);
-      }
-      e[i] = s1;
-      e2[i] = s2;
-    }
-    transpose_reduce<LPR, R>(e, c);
-    transpose_reduce<LPR, R>(e2, c);
     double racc[RPL], racc2[RPL];
 #pragma unroll
-    for (int m = 0; m < RPL; ++m) {
-      racc[m] = e[m];
-      racc2[m] = e2[m];
+    for (int m = 0; m < RPL; ++m) racc[m] = racc2[m] = 0.0;
+#pragma unroll
+    for (int h = 0; h < CPB; ++h) {
+      const int64_t col = (ch0 + h) * J + (int64_t)c * V;
+      const bool cval = col < d;
+      float gv[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) gv[v] = cval ? a.guess0[col + v] : 0.f;
+      float e[R], e2[R];
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const float t = x[h][i][v] - gv[v];
+          s1 = fmaf(t, t, s1);
+          s2 = fmaf(x[h][i][v], x[h][i][v], s2);
+        }
+        e[i] = s1;
+        e2[i] = s2;
+      }
+      transpose_reduce<LPR, R>(e, c);
+      transpose_reduce<LPR, R>(e2, c);
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) {
+        racc[m] += (double)e[m];
+        racc2[m] += (double)e2[m];
+      }
     }
     publish(0, racc, racc2, 0.0, fin ? (double)(gcur * gcur) : 0.0);
   }
-  if (!grid_sync(a.bar, nb, gen, &s_ok)) return;
 
   int64_t it = 0;
   double last_mv = NAN;
@@ -198,38 +231,36 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   uint64_t prev_ = __builtin_amdgcn_s_memrealtime();
 #endif
   for (;; ++it) {
-    // (1) reduce the previous pass's partials, same order in every block: the
-    // slab columns needed (D2, at it = 0 also r, then mv2 / gn2) are spread over
-    // G thread groups that each sum every G-th block row; the G partials are
-    // then combined in LDS in group order (deterministic, and G loads in flight
-    // per column instead of nb dependent ones).
+    // (1) gather pass `it` (INIT at it = 0): D2 (+ r at it = 0) and the per-wave
+    // movement / norm partials, summed over blocks in block order
     {
-      const double* sl = a.slab + (int64_t)(it & 1) * nb * S;
-      const int64_t ncol = (it == 0 ? 2 * K : K) + 2;      // [D2 | (r) | mv2 gn2]
-      const int64_t span = ncol <= 64 ? 64 : ncol <= 128 ? 128 : ncol <= 256 ? 256
-                          : ncol <= 512 ? 512 : 1024;
-      const int G = (int)(blockDim.x / span) > 0 ? (int)(blockDim.x / span) : 1;
-      for (int64_t col0 = 0; col0 < ncol; col0 += span) {
-        const int g = tid / (int)span;
-        const int64_t cc = col0 + tid % span;
-        const int64_t src = cc < ncol - 2 ? cc : 2 * K + (cc - (ncol - 2));
-        double s = 0.0;
-        if (g < G && cc < ncol)
-          for (unsigned b = g; b < nb; b += G) s += sl[(int64_t)b * S + src];
-        __syncthreads();
-        if (g < G) s_part[g * span + tid % span] = s;
-        __syncthreads();
-        if (tid < span && col0 + tid < ncol) {
-          double t = 0.0;
-          for (int gg = 0; gg < G; ++gg) t += s_part[gg * span + tid];
-          const int64_t c2 = col0 + tid;
-          if (c2 < K) s_d2[c2] = t;
-          else if (c2 < ncol - 2) s_r[c2 - K] = t;
-          else s_tot[c2 - (ncol - 2)] = t;
-        }
+      const gu64* in = gran + (it & 1) * nb * 2 * NV;
+      const unsigned tag = (unsigned)(it + 1);
+      const int64_t nk = it == 0 ? 2 * K : K;
+      const int64_t ncol = nk + 2 * NW;
+      bool ok = true;
+      for (int64_t cc = tid; cc < ncol; cc += blockDim.x) {
+        const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
+        double sum;
+        if (!gather_value(in + 2 * v, 2 * NV, nb, tag, tmo, sum)) { ok = false; break; }
+        if (cc < K) s_d2[cc] = sum;
+        else if (cc < nk) s_r[cc - K] = sum;
+        else s_wp[cc - nk] = sum;
       }
+      if (!ok) s_ok = 0;
+      __syncthreads();
+      if (s_ok == 0) return;                       // timed out: every thread leaves
+      if (tid == 0) {
+        double m = 0.0, g = 0.0;
+        for (int ww = 0; ww < NW; ++ww) {
+          m += s_wp[2 * ww];
+          g += s_wp[2 * ww + 1];
+        }
+        s_tot[0] = m;
+        s_tot[1] = g;
+      }
+      __syncthreads();
     }
-    __syncthreads();
     RES_T(0)
     // (2) tol test of the pass that produced g_it (M:180-183)
     if (it >= 1) {
@@ -239,8 +270,42 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
     }
     if (it == a.maxiter) break;
 
-    // (3) coefficients for pass `it`
-    if (a.mode == 0) {
+    // (3) coefficients for pass `it`: one wave, lane = client, when K <= 64
+    if (K <= 64) {
+      if (w == 0) {
+        const int k = lane;
+        const bool kv = k < K;
+        if (a.mode == 0) {
+          const double wk = kv ? 1.0 / (double)clamp_dist(s_d2[k], a.eps) : 0.0;
+          const double W = wave_sum(wk);
+          if (kv) s_coef[k] = (float)(wk / W);
+          if (lane == 0) s_anoise = 0.f;
+        } else {
+          const float s = sqrtf((float)(s_tot[1] / (double)d));      // M:146
+          const float thr = (s * s) * 500.0f;                         // M:152
+          const double s2 = (double)s * (double)s;
+          double ck = 0.0;
+          if (kv) {
+            float n4[4];
+            normal4(a.seed, kStreamChannel, (uint64_t)it, (uint64_t)k, n4);
+            const float hr = n4[0] * 0.70710678118654752f, hi = n4[1] * 0.70710678118654752f;
+            const float h2 = hr * hr + hi * hi;                       // M:403
+            const float dist = clamp_dist(s_d2[k], a.eps);
+            const double dd = (double)dist;
+            const double pk = (s_r[k] + s2) / (dd * dd * (double)(d + 1)) / (double)h2;   // M:404
+            const double pup = pk != pk ? pk : fmax(pk, (double)thr);  // M:405
+            ck = sqrt(a.P_max / pup) / dd;                            // M:407
+          }
+          const double Sc = wave_sum(ck);
+          const double nd = a.has_noise ? a.noise_sd * (double)normal1(a.seed, kStreamNoise,
+                                                                       (uint64_t)it, (uint64_t)d)
+                                        : 0.0;
+          const double scale = (double)s / ((double)s * Sc + nd);     // M:153-155
+          if (kv) s_coef[k] = (float)(ck * scale);
+          if (lane == 0) s_anoise = a.has_noise ? (float)(scale * a.noise_sd) : 0.f;
+        }
+      }
+    } else if (a.mode == 0) {
       double wsum = 0.0;
       for (int64_t k = tid; k < K; k += blockDim.x) wsum += 1.0 / (double)clamp_dist(s_d2[k], a.eps);
       const double W = block_sum(wsum, scratch);
@@ -259,9 +324,9 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         const float h2 = hr * hr + hi * hi;                       // M:403
         const float dist = clamp_dist(s_d2[k], a.eps);
         const double dd = (double)dist;
-        const double p = (s_r[k] + s2) / (dd * dd * (double)(d + 1)) / (double)h2;   // M:404
-        const double pup = p != p ? p : fmax(p, (double)thr);     // M:405
-        const double ck = sqrt(a.P_max / pup) / dd;               // M:407
+        const double pk = (s_r[k] + s2) / (dd * dd * (double)(d + 1)) / (double)h2;   // M:404
+        const double pup = pk != pk ? pk : fmax(pk, (double)thr);  // M:405
+        const double ck = sqrt(a.P_max / pup) / dd;                // M:407
         s_coef[k] = (float)ck;
         csum += ck;
       }
@@ -277,31 +342,34 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
     __syncthreads();
     RES_T(1)
 
-    // (4) phase A on the resident tile
+    // (4) phase A on the resident tiles
     float wt[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const int64_t k = rg + (int64_t)NRG * i;
       wt[i] = k < K ? s_coef[k] : 0.f;
     }
-    float acc[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) acc[v] = 0.f;
+    for (int h = 0; h < CPB; ++h) {
+      float acc[V];
 #pragma unroll
-    for (int i = 0; i < R; ++i)
+      for (int v = 0; v < V; ++v) acc[v] = 0.f;
 #pragma unroll
-      for (int v = 0; v < V; ++v) acc[v] = fmaf(wt[i], x[i][v], acc[v]);
+      for (int i = 0; i < R; ++i)
 #pragma unroll
-    for (int o = LPR; o < 64; o <<= 1)
+        for (int v = 0; v < V; ++v) acc[v] = fmaf(wt[i], x[h][i][v], acc[v]);
 #pragma unroll
-      for (int v = 0; v < V; ++v) acc[v] += __shfl_xor(acc[v], o, 64);
-    if (q == 0) {
+      for (int o = LPR; o < 64; o <<= 1)
 #pragma unroll
-      for (int v = 0; v < V; ++v) s_red[w][c * V + v] = acc[v];
+        for (int v = 0; v < V; ++v) acc[v] += __shfl_xor(acc[v], o, 64);
+      if (q == 0) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) s_red[w][h * J + c * V + v] = acc[v];
+      }
     }
     __syncthreads();
     double mvp = 0.0, gnp = 0.0;
-    if (tid < J) {
+    if (tid < JB) {
       float gnew = 0.f;
       if (fin) {
         float sum = 0.f;
@@ -319,36 +387,39 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
     }
     __syncthreads();
     RES_T(2)
-    // (5) phase B: distances to the new iterate
-    float gv[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) gv[v] = s_g[c * V + v];
-    float e[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      float s1 = 0.f;
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const float t = x[i][v] - gv[v];
-        s1 = fmaf(t, t, s1);
-      }
-      e[i] = s1;
-    }
-    transpose_reduce<LPR, R>(e, c);
+    // (5) phase B: distances to the new iterate, every chunk, fp64 across chunks
     double racc[RPL];
 #pragma unroll
-    for (int m = 0; m < RPL; ++m) racc[m] = e[m];
+    for (int m = 0; m < RPL; ++m) racc[m] = 0.0;
+#pragma unroll
+    for (int h = 0; h < CPB; ++h) {
+      float gv[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) gv[v] = s_g[h * J + c * V + v];
+      float e[R];
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        float s1 = 0.f;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const float t = x[h][i][v] - gv[v];
+          s1 = fmaf(t, t, s1);
+        }
+        e[i] = s1;
+      }
+      transpose_reduce<LPR, R>(e, c);
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) racc[m] += (double)e[m];
+    }
     RES_T(3)
-    publish((int)((it + 1) & 1), racc, nullptr, mvp, gnp);
+    publish(it + 1, racc, nullptr, mvp, gnp);
     RES_T(4)
-    if (!grid_sync(a.bar, nb, gen, &s_ok)) return;
-    RES_T(5)
   }
 #ifdef GMK_RES_PROF
   if (blockIdx.x == 0 && threadIdx.x == 0)
-    printf("GMK_RES_PROF nb=%u iters=%ld ns/iter: reduce %.0f coef %.0f phaseA %.0f phaseB %.0f "
-           "publish %.0f barrier %.0f\n", nb, (long)it, 10.0 * prof_[0] / it, 10.0 * prof_[1] / it,
-           10.0 * prof_[2] / it, 10.0 * prof_[3] / it, 10.0 * prof_[4] / it, 10.0 * prof_[5] / it);
+    printf("GMK_RES_PROF nb=%u CPB=%d iters=%ld ns/iter: gather %.0f coef %.0f phaseA %.0f "
+           "phaseB %.0f publish %.0f\n", nb, CPB, (long)it, 10.0 * prof_[0] / it,
+           10.0 * prof_[1] / it, 10.0 * prof_[2] / it, 10.0 * prof_[3] / it, 10.0 * prof_[4] / it);
 #endif
 
   if (fin) a.out[gj] = gcur;
@@ -362,14 +433,31 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
 
 // ---------------------------------------------------------------------------
 
-template <int V, int NW, int LPR, int R>
-static const void* res_fn() {
-  return reinterpret_cast<const void*>(&weiszfeld_resident<V, NW, LPR, R>);
+// Chunks per block: CPB * J columns must map one finisher column per thread, and
+// the tile x[CPB][R][V] must stay within 64 VGPRs.
+constexpr bool res_cpb_ok(int V, int NW, int LPR, int R, int CPB) {
+  return CPB == 1 || (CPB * LPR * V <= NW * 64 && CPB * R * V <= 64);
 }
 
-static const void* resident_kernel(const PassCfg& cfg) {
-#define GMK_RES(V_, W_, L_, R_) \
-  if (cfg.V == V_ && cfg.NW == W_ && cfg.LPR == L_ && cfg.R == R_) return res_fn<V_, W_, L_, R_>();
+template <int V, int NW, int LPR, int R, int CPB>
+static const void* res_fn() {
+  if constexpr (res_cpb_ok(V, NW, LPR, R, CPB))
+    return reinterpret_cast<const void*>(&weiszfeld_resident<V, NW, LPR, R, CPB>);
+  else
+    return nullptr;
+}
+
+static const void* resident_kernel(const PassCfg& cfg, int cpb) {
+#define GMK_RES(V_, W_, L_, R_)                                              \
+  if (cfg.V == V_ && cfg.NW == W_ && cfg.LPR == L_ && cfg.R == R_) {         \
+    switch (cpb) {                                                           \
+      case 1: return res_fn<V_, W_, L_, R_, 1>();                            \
+      case 2: return res_fn<V_, W_, L_, R_, 2>();                            \
+      case 4: return res_fn<V_, W_, L_, R_, 4>();                            \
+      case 8: return res_fn<V_, W_, L_, R_, 8>();                            \
+      default: return nullptr;                                               \
+    }                                                                        \
+  }
 #define GMK_RES_V(V_)                                                                         \
   GMK_RES(V_, 16, 64, 1) GMK_RES(V_, 16, 64, 2) GMK_RES(V_, 16, 64, 4) GMK_RES(V_, 16, 64, 8)   \
   GMK_RES(V_, 16, 32, 8) GMK_RES(V_, 16, 16, 8) GMK_RES(V_, 16, 8, 8) GMK_RES(V_, 16, 4, 8)
@@ -381,16 +469,40 @@ static const void* resident_kernel(const PassCfg& cfg) {
   return nullptr;
 }
 
-int resident_max_blocks(const PassCfg& cfg, int num_cu) {
-  const void* fn = resident_kernel(cfg);
+// Blocks of CPB chunks each: the fewest blocks (largest valid CPB) up to 8 chunks
+// per block while more than kResTargetBlocks blocks remain; GMAGG_RES_CPB=n forces
+// n (A/B).  Returns false when the grid cannot be co-resident.
+constexpr int kResTargetBlocks = 16;
+
+bool resident_plan(const PassCfg& cfg, int64_t nch, int num_cu, int* cpb_out, int* nb_out) {
+  int cpb = 0;
+  if (const char* e = getenv("GMAGG_RES_CPB")) {
+    cpb = atoi(e);
+    if (!resident_kernel(cfg, cpb)) return false;
+  } else {
+    for (int c = 1; c <= 8; c *= 2) {
+      if (!resident_kernel(cfg, c)) break;
+      cpb = c;
+      if ((nch + c - 1) / c <= kResTargetBlocks) break;
+    }
+  }
+  if (cpb == 0) return false;
+  const void* fn = resident_kernel(cfg, cpb);
   int n = 0;
-  if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, cfg.NW * 64, 0) != hipSuccess)
-    return 0;
-  return n * num_cu;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, cfg.NW * 64, 0) != hipSuccess) return false;
+  const int64_t nb = (nch + cpb - 1) / cpb;
+  if (nb > (int64_t)n * num_cu) return false;
+  *cpb_out = cpb;
+  *nb_out = (int)nb;
+  return true;
 }
 
-hipError_t launch_resident(const PassCfg& cfg, int grid, const ResArgs& a, hipStream_t s) {
-  const void* fn = resident_kernel(cfg);
+size_t resident_gran_words(int64_t K, const PassCfg& cfg, int nb) {
+  return (size_t)2 * nb * 2 * (size_t)(2 * K + 2 * cfg.NW);
+}
+
+hipError_t launch_resident(const PassCfg& cfg, int cpb, int grid, const ResArgs& a, hipStream_t s) {
+  const void* fn = resident_kernel(cfg, cpb);
   if (!fn) return hipErrorInvalidValue;
   void* args[] = {const_cast<ResArgs*>(&a)};
   return hipLaunchCooperativeKernel(fn, dim3(grid), dim3(cfg.NW * 64), args, 0, s);

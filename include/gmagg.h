@@ -117,7 +117,8 @@ typedef struct gm_result {
     int32_t converged;        /* 1 if the loop exited through the tol test */
     int32_t algo_used;        /* gm_algo actually run */
     int32_t guard;            /* gm_guard: what the Gram accuracy guard decided */
-    int32_t reserved;
+    int32_t gram_kind;        /* Gram runs: 1 scaled f16 split (3 MFMA products), 2 bf16 split
+                                 (4 products, after an f16 range overflow), 3 f32-input; else 0 */
 } gm_result;
 
 typedef struct gm_ctx gm_ctx;

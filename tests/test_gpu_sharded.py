@@ -74,7 +74,7 @@ def _sharded(X, p, P, opts, aircomp, check_every=0, algo=0, panels=False):
                                                 g0.data_ptr(), res.data_ptr(), C.byref(o),
                                                 C.byref(rr), None), "sharded gm")
             torch.cuda.synchronize(dev)
-            out[r] = (lo, hi, res, rr.iters, rr.algo_used)
+            out[r] = (lo, hi, res, rr.iters, rr.algo_used, rr.guard)
         except Exception as e:  # noqa: BLE001
             errs.append(e)
             barrier.abort()
@@ -88,7 +88,8 @@ def _sharded(X, p, P, opts, aircomp, check_every=0, algo=0, panels=False):
     full = torch.empty(d, device=dev)
     iters = {o_[3] for o_ in out}
     _sharded.algos = {o_[4] for o_ in out}
-    for lo, hi, res, _, _ in out:
+    _sharded.guards = {o_[5] for o_ in out}
+    for lo, hi, res, _, _, _ in out:
         full[lo:hi] = res
     return full, iters
 
@@ -169,8 +170,11 @@ def test_sharded_gram_equals_unsharded(algo):
     got, iters = _sharded(X, p, P, opts, aircomp=False, algo=algo)
     assert len(iters) == 1 and abs(iters.pop() - n) <= 1
     assert len(_sharded.algos) == 1
+    info = (_sharded.algos, _sharded.guards, bz.aggregators.last_result)
     if algo == 3:
-        assert _sharded.algos == {_lib.GM_ALGO_GRAM}
+        bz.gm2(X, dict(opts, guess=p, algo="gram"))
+        info = info + (bz.aggregators.last_result,)
+        assert _sharded.algos == {_lib.GM_ALGO_GRAM}, info
     assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-5
 
 

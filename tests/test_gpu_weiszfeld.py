@@ -388,3 +388,44 @@ def test_gram_guard_falls_back_to_streaming(case):
     assert rel_l2(got.cpu().numpy(), want.numpy()) <= TOL
     if res.converged and tr.iters < 30:
         assert abs(res.iters - tr.iters) <= ITER_SLACK
+
+
+def test_gram_f16_split_matches_bf16_split(monkeypatch):
+    """The scaled f16 split (3 MFMA products, default) and the bf16 split (4
+    products) give the same aggregate and iterations on the C4 recipe."""
+    m = bz()
+    X, g0 = _c4_like(256, 1 << 20, seed=777)
+    a = m.gm2(X, {"maxiter": 1000, "guess": g0, "algo": "gram"})
+    ra = m.aggregators.last_result
+    monkeypatch.setenv("GMAGG_GRAM_KIND", "bf16")
+    b = m.gm2(X, {"maxiter": 1000, "guess": g0, "algo": "gram"})
+    rb = m.aggregators.last_result
+    assert (ra.gram_kind, rb.gram_kind) == ("f16_split", "bf16_split")
+    assert ra.guard == rb.guard == "accepted" and ra.iters == rb.iters
+    assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 1e-6
+
+
+@pytest.mark.parametrize("spike", [1e6, float("inf")])
+def test_gram_f16_range_overflow_falls_back(spike):
+    """An element far beyond the f16 headroom of its row's scale (set from the
+    block's first stages) makes the f16 Gram non-finite: the call reruns the bf16
+    split (or, for a non-finite input, ends on the streaming path) and still
+    matches the reference."""
+    m = bz()
+    g = torch.Generator().manual_seed(5)
+    K, d = 64, 1 << 18
+    X = 0.05 * torch.randn(K, d, generator=g)
+    X[K - 12:] += 0.25
+    X[5, 200_000] = spike                     # well past the first stages of its block
+    p = torch.zeros(d)
+    opts = {"maxiter": 1000, "tol": 1e-5, "guess": p}
+    want, tr = orc.gm2(X.clone(), dict(opts))
+    got = m.gm2(X.cuda(), dict(opts, guess=p.cuda(), algo="gram"))
+    res = m.aggregators.last_result
+    if spike == float("inf"):
+        assert res.algo == "stream" and res.guard == "rejected"
+        assert torch.equal(torch.isnan(got.cpu()), torch.isnan(want))
+        return
+    assert res.algo == "gram" and res.gram_kind == "bf16_split"
+    assert rel_l2(got.cpu().numpy(), want.numpy()) <= TOL
+    assert abs(res.iters - tr.iters) <= ITER_SLACK
