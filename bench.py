@@ -49,7 +49,10 @@ WORKLOADS = {
     "c4": (256, 125_000_000, 51, "gm2", None),          # the whole C4 job (d-sharded over N)
     "c5-problem": (50, 100_000, 10, "gm2", None),
     "c2": (50, 7850, 10, "gm", 1e-2),                   # MNIST MLP d, K=50, B=10, AirComp gm
+    "c5": (50, 100_000, 10, "gm2", None),               # the batched sweep (run_c5)
 }
+C5_VARS = (0.0, 1e-3, 1e-2, 1e-1)
+C5_BYZ = (0, 5, 10)
 MFMA_F32_PEAK_TFLOPS = 157.3                 # v_mfma_f32_32x32x2_f32, dense (MI355X_MICROARCH.md)
 MFMA_BF16_PEAK_TFLOPS = 2516.6               # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz, dense
 
@@ -57,8 +60,8 @@ MFMA_BF16_PEAK_TFLOPS = 2516.6               # 256 CU x 4 SIMD x 1024 FLOP/clk x
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=None, help="default 20 (c5: 2 sweeps)")
+    p.add_argument("--warmup", type=int, default=None, help="default 3 (c5: 1 sweep)")
     p.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     p.add_argument("--algo", default="auto", choices=["auto", "stream", "twopass", "gram", "gram_f32"])
     p.add_argument("--agg", default=None, choices=["gm2", "gm"],
@@ -86,11 +89,20 @@ def parse():
                         "(its columns, its per-iteration exchange over a 1-rank communicator): "
                         "the per-rank time of the N=P run minus the cross-GPU all-reduce latency. "
                         "Convergence uses the shard's sums only, so iters may differ from N=P.")
+    p.add_argument("--problems", type=int, default=4096, help="c5: problems per sweep")
+    p.add_argument("--reading", default="prenoise", choices=["prenoise", "aircomp"],
+                   help="c5: var > 0 as the reference's `--agg gm2 --var v` (OMA pre-noise, then "
+                        "gm2; M:351-353) or as the AirComp gm aggregator (M:131-160)")
     p.add_argument("--one-gpu", action="store_true",
                    help="N>1 rehearsal on a one-GPU box: every rank on cuda:0, gloo process "
                         "group, the torch all-reduce callback instead of RCCL (timing is not "
                         "a scaling measurement)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.steps is None:
+        a.steps = 2 if a.workload == "c5" else 20
+    if a.warmup is None:
+        a.warmup = 1 if a.workload == "c5" else 3
+    return a
 
 
 def host_cpu_share() -> int:
@@ -189,6 +201,162 @@ def cpu_baseline(X, g0, agg, var, iters, d_full, budget, max_cols):
                        + ("" if dc == d_full else ", linear in d (extrapolated)"))}
 
 
+def run_c5(args, json_out):
+    """BASELINE config C5: a draw.ipynb-style Monte-Carlo sweep of `args.problems`
+    independent K=50 x d=100k aggregations over var in {0, 1e-3, 1e-2, 1e-1} x
+    B in {0, 5, 10}.  One step = the whole sweep: per var group (problems/4 each,
+    in batches of <= 1024) one batched call, and for var > 0 in the `prenoise`
+    reading (the reference's `--agg gm2 --var v`, M:351-353) the batched OMA
+    pre-noise (M:385-394) first — both inside the timed region.  Inputs are
+    regenerated on the device (untimed) before every step, since OMA is in place."""
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd import _lib
+    from byzantine_aircomp_amd.batched import gm2_batched, gm_batched, oma_batched
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    K, d, _, _, _ = WORKLOADS["c5"]
+    ctx = bz.context(dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    per_var = args.problems // len(C5_VARS)
+    chunk = min(1024, per_var)
+    groups = []                      # (var, X [P, K, d], g0 [P, d])
+    for vi, var in enumerate(C5_VARS):
+        for c0 in range(0, per_var, chunk):
+            P = min(chunk, per_var - c0)
+            groups.append((vi, var, c0, torch.empty(P, K, d, device=dev),
+                           torch.empty(P, d, device=dev)))
+
+    def fill():
+        for vi, var, c0, X, g0 in groups:
+            for p in range(X.shape[0]):
+                B = C5_BYZ[(c0 + p) % 3]
+                _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, X[p].data_ptr(), K, d, d, B, 0.0,
+                                                       0.05, 0.25, 0.5, 1000 * vi + c0 + p, stream),
+                           "fill")
+            _lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), g0.numel(), 0.0, 0.01,
+                                                  777 + vi + c0, stream), "fill")
+        torch.cuda.synchronize(dev)
+
+    def step(reading):
+        iters, per_group = [], {}
+        for vi, var, c0, X, g0 in groups:
+            opts = {"maxiter": args.maxiter, "tol": 1e-5, "guess": g0}
+            t0 = time.perf_counter()
+            if var == 0.0:
+                _, res = gm2_batched(X, opts)
+            elif reading == "prenoise":
+                oma_batched(X, var, seed=31 + vi * 1000 + c0)
+                _, res = gm2_batched(X, opts)
+            else:
+                _, res = gm_batched(X, dict(opts, noise_var=var, seed=31 + vi * 1000 + c0))
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
+            its = [r.iters for r in res]
+            iters += its
+            g = per_group.setdefault(var, {"seconds": 0.0, "problems": 0, "iters": 0})
+            g["seconds"] += dt
+            g["problems"] += len(its)
+            g["iters"] += sum(its)
+        return iters, per_group
+
+    def measure(reading, steps, warmup):
+        for _ in range(warmup):
+            fill()
+            step(reading)
+        total, pass_ms, launches, iters, groups_out = 0.0, 0.0, 0, [], {}
+        for _ in range(steps):
+            fill()
+            ctx.pass_timing(True)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            iters, groups_out = step(reading)
+            torch.cuda.synchronize(dev)
+            total += time.perf_counter() - t0
+            ms, n = ctx.pass_timing(False)
+            pass_ms += ms
+            launches += n
+        return total, pass_ms, launches, iters, groups_out
+
+    total, pass_ms, launches, iters, per_group = measure(args.reading, args.steps, args.warmup)
+    n_prob = len(iters)
+    mean_it = sum(iters) / n_prob
+    step_bytes = sum(iters) * 4.0 * K * d            # algorithmic STEP-pass bytes per sweep
+    achieved = step_bytes * args.steps / (pass_ms / 1e3) / 1e9 if pass_ms > 0 else None
+    agg_bytes = sum(i + 1 for i in iters) * 4.0 * K * d
+    alt_reading = "aircomp" if args.reading == "prenoise" else "prenoise"
+    alt = None
+    if args.alt_steps != 0:
+        a_total, _, _, a_iters, a_groups = measure(alt_reading, 1, 0)
+        alt = {"reading": alt_reading, "value": len(a_iters) / a_total, "seconds": a_total,
+               "mean_iters": sum(a_iters) / len(a_iters),
+               "groups": {str(k): {"problems_per_s": v["problems"] / v["seconds"],
+                                   "mean_iters": v["iters"] / v["problems"]}
+                          for k, v in a_groups.items()}}
+    cpu = None
+    if not args.no_cpu:
+        cpu = c5_cpu_baseline(groups[0][3][0], groups[0][4][0], mean_it, n_prob, args.cpu_budget)
+    line = {
+        "metric": METRIC, "value": n_prob * args.steps / total, "unit": "aggregations/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * total / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (Philox on device: honest N(0,0.05^2), B rows N(0.25,0.5^2), "
+                "guess N(0,0.01^2))",
+        "config": {"workload": f"c5: {n_prob} independent gm2 problems K={K} x d={d} fp32 over "
+                               f"var {list(C5_VARS)} x B {list(C5_BYZ)}, reading '{args.reading}'"
+                               + (" (OMA pre-noise then gm2, M:351-353)"
+                                  if args.reading == "prenoise" else " (AirComp gm for var > 0)"),
+                   "K": K, "d": d, "problems": n_prob, "mean_iters": mean_it,
+                   "parallelism": "batched (one launch per pass covers every problem of a group)",
+                   "groups": {str(k): {"problems_per_s": v["problems"] / v["seconds"],
+                                       "mean_iters": v["iters"] / v["problems"]}
+                              for k, v in per_group.items()}},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
+                     "kernel": "weiszfeld_pass (batched STEP, blockIdx.y = problem)",
+                     "launches_timed": launches, "avg_launch_us": 1e3 * pass_ms / max(launches, 1),
+                     "algorithmic_bytes": "4*K*d per problem per Weiszfeld iteration (sum over "
+                                          "problems of iters) / summed STEP launch time",
+                     "aggregation_frac": agg_bytes / (total / args.steps) / 1e9 / HBM_PEAK_GBS,
+                     "aggregation_frac_def": "sum_p 4*K*d*(iters_p+1) / ms_per_step / 8 TB/s "
+                                             "(OMA pre-noise time included, its bytes not)"},
+        "cpu_baseline": cpu,
+        "check": {"what": "every problem ran to its own tol test or maxiter",
+                  "max_iters": max(iters), "min_iters": min(iters)},
+        "alt_layout": alt,
+    }
+    print(json.dumps(line), file=json_out, flush=True)
+
+
+def c5_cpu_baseline(X, g0, mean_iters, problems, budget):
+    """Oracle gm2 (op-for-op torch-CPU restatement of M:162-184) on ONE C5 problem
+    (K=50 x d=100k, the same data as GPU problem 0), tol disabled, a bounded number
+    of iterations; scaled to the sweep's mean iteration count x its problem count
+    (the OMA pre-noise of the var > 0 groups is not added: the CPU figure is a
+    lower bound on the reference's time)."""
+    from oracle import aggregators as orc
+    threads = host_cpu_share()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        Xc, gc = X.cpu(), g0.cpu()
+        t0 = time.perf_counter()
+        orc.gm2(Xc, {"maxiter": 1, "tol": -1.0, "guess": gc})
+        t1 = time.perf_counter() - t0
+        n = max(1, min(200, int(budget / max(t1, 1e-6))))
+        t0 = time.perf_counter()
+        orc.gm2(Xc, {"maxiter": n, "tol": -1.0, "guess": gc})
+        tn = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    per_problem = tn / n * (mean_iters + 1)
+    return {"value": 1.0 / per_problem, "unit": "aggregations/s", "cores": threads, "kind": "port",
+            "host_cpus_visible": os.cpu_count(),
+            "sample": f"oracle gm2 (torch CPU, {threads} threads) on one K=50 x d=100000 problem: "
+                      f"{n} iterations in {tn:.2f} s; scaled to {mean_iters + 1:.2f} passes per "
+                      f"problem (the sweep's mean); {problems} problems take {problems * per_problem:.0f} s"}
+
+
 def main():
     args = parse()
     # stdout carries exactly one JSON line: everything else written to fd 1 (RCCL's
@@ -198,6 +366,10 @@ def main():
     os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.workload == "c5":
+        if world != 1:
+            raise SystemExit("c5 is a one-GPU batched sweep (problems are independent)")
+        return run_c5(args, json_out)
     local = 0 if args.one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")

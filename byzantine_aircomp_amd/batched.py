@@ -18,7 +18,7 @@ import torch
 from . import _lib
 from .aggregators import GMResult, _ALGO_NAMES, _seed, _stream_ptr, context
 
-__all__ = ["gm2_batched", "gm_batched", "SEED_STRIDE"]
+__all__ = ["gm2_batched", "gm_batched", "oma_batched", "SEED_STRIDE"]
 
 SEED_STRIDE = 0x9E3779B97F4A7C15
 
@@ -61,6 +61,21 @@ def _run(X: torch.Tensor, options: dict, aircomp: bool):
     results = [GMResult(r.iters, r.last_movement, bool(r.converged),
                         _ALGO_NAMES.get(r.algo_used, "?")) for r in res]
     return out, results
+
+
+def oma_batched(X: torch.Tensor, noise_var: float, seed: int = 2021) -> torch.Tensor:
+    """OMA pre-noise (M:385-394) in place on each of P problems X[p] ([P, K, d]):
+    the reference's `--agg gm2 --var v` path adds it before gm2 (M:351-352).
+    Problem p's draws equal `aggregators.OMA(X[p], noise_var, seed + p * SEED_STRIDE)`."""
+    if X.dim() != 3 or X.device.type != "cuda" or X.dtype != torch.float32 or X.stride(2) != 1:
+        raise TypeError("oma_batched needs an fp32 CUDA [P, K, d] tensor with unit column stride")
+    P, K, d = X.shape
+    ctx = context(X.device)
+    with torch.cuda.device(X.device):
+        _lib.check(ctx.lib.gm_oma_philox_batched_f32(
+            ctx.handle, X.data_ptr(), P, K, d, X.stride(1), X.stride(0), float(noise_var),
+            int(seed) & 0xFFFFFFFFFFFFFFFF, _stream_ptr(X.device)), "gm_oma_philox_batched_f32")
+    return X
 
 
 def gm2_batched(X, options=None):

@@ -978,6 +978,42 @@ int gm_mean_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, fl
   return GM_OK;
 }
 
+int gm_honest_variance_f32(gm_ctx* c, const float* X, int64_t honest, int64_t d, int64_t ldx,
+                           float* out, void* stream) {
+  if (!c || !X || !out || honest < 1 || d < 1 || ldx < d)
+    return fail(GM_ERR_INVALID, "gm_honest_variance_f32: bad args");
+  const int wshift = 0;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  WsOrder order(c, s);
+  HIPCHK(order.err);
+  const int nb = honest_var_blocks(d, c->num_cu);
+  Workspace w;
+  const int rc = ensure_ws(c, 1, 1, nb, &w);
+  if (rc) return rc;
+  HIPCHK(launch_honest_var(X, honest, d, ldx, wshift, nb, w.slab, out, s));
+  return GM_OK;
+}
+
+int gm_honest_variance_panels_f32(gm_ctx* c, const float* X, int64_t K, int64_t honest, int64_t d,
+                                  int64_t panel_stride, float* out, void* stream) {
+  const int64_t W = gm_panel_width(K);
+  if (!c || !X || !out || honest < 1 || honest > K || d < 1 || W == 0 || panel_stride < K * W)
+    return fail(GM_ERR_INVALID, "gm_honest_variance_panels_f32: bad args");
+  int wshift = 0;
+  while ((int64_t)1 << wshift < W) ++wshift;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  WsOrder order(c, s);
+  HIPCHK(order.err);
+  const int nb = honest_var_blocks(d, c->num_cu);
+  Workspace w;
+  const int rc = ensure_ws(c, 1, 1, nb, &w);
+  if (rc) return rc;
+  HIPCHK(launch_honest_var(X, honest, d, panel_stride, wshift, nb, w.slab, out, s));
+  return GM_OK;
+}
+
 int gm_median_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, float* out,
                   void* stream) {
   if (!c || !X || !out || K < 1 || d < 0 || ldx < d) return fail(GM_ERR_INVALID, "gm_median_f32: bad args");
@@ -1033,6 +1069,20 @@ int gm_oma_philox_f32(gm_ctx* c, float* X, int64_t K, int64_t d, int64_t ldx, do
   const int64_t col_off = c->d_total > 0 ? c->d_offset : 0;
   HIPCHK(launch_oma_philox(X, K, d, ldx, d_total, col_off, (float)std::sqrt(noise_var), seed,
                            reinterpret_cast<hipStream_t>(stream)));
+  return GM_OK;
+}
+
+int gm_oma_philox_batched_f32(gm_ctx* c, float* X, int64_t P, int64_t K, int64_t d, int64_t ldx,
+                              int64_t pstride, double noise_var, uint64_t seed, void* stream) {
+  if (!c || !X || P < 0 || K < 0 || d < 0 || ldx < d || noise_var < 0 ||
+      (P > 1 && pstride < K * ldx))
+    return fail(GM_ERR_INVALID, "gm_oma_philox_batched_f32: bad args");
+  if (P == 0 || K == 0 || d == 0) return GM_OK;
+  if (c->d_total > 0)
+    return fail(GM_ERR_UNSUPPORTED, "gm_oma_philox_batched_f32: not on a d-sharded context");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(launch_oma_philox(X, K, d, ldx, d, 0, (float)std::sqrt(noise_var), seed,
+                           reinterpret_cast<hipStream_t>(stream), 0, P, P > 1 ? pstride : 0));
   return GM_OK;
 }
 

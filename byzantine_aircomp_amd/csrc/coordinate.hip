@@ -49,6 +49,89 @@ __global__ void __launch_bounds__(256) col_mean(const float* __restrict__ X, int
   }
 }
 
+// getVarience (M:127-129): mean over the H honest rows of ||h_k - mean_k h||^2
+// = (1/H) sum_j sum_k (h_kj - m_j)^2, in ONE streaming pass: per column the sums
+// of (h_kj - h_0j) and of its square in fp64 (shifted by the column's first row:
+// no cancellation for data far from 0), var_j = b - a^2/H; block partials in fp64,
+// summed in a fixed order by honest_var_final.  W columns per thread as in
+// col_mean (W = 4: float4 rows).  wshift > 0: X in the panel layout
+// [ceil(d/2^wshift)][K][2^wshift], ldx = the panel stride (a float4 group never
+// straddles a panel).
+template <int W>
+__global__ void __launch_bounds__(256) honest_var_part(const float* __restrict__ X, int64_t H,
+                                                       int64_t d, int64_t ldx, int wshift,
+                                                       double* __restrict__ part) {
+  typedef float fv __attribute__((ext_vector_type(W)));
+  __shared__ double scratch[16];
+  constexpr int U = 8;
+  const int64_t G = d / W;
+  double acc = 0.0;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j0 = g * W;
+    const float* col = wshift ? X + (j0 >> wshift) * ldx + (j0 & ((1 << wshift) - 1)) : X + j0;
+    const int64_t rs = wshift ? ((int64_t)1 << wshift) : ldx;        // row stride
+    const fv c = *reinterpret_cast<const fv*>(col);
+    double a[W], b[W];
+#pragma unroll
+    for (int v = 0; v < W; ++v) a[v] = b[v] = 0.0;
+    int64_t k = 0;
+    for (; k + U <= H; k += U) {
+      fv x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        x[u] = __builtin_nontemporal_load(reinterpret_cast<const fv*>(col + (k + u) * rs));
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int v = 0; v < W; ++v) {
+          const double t = (double)x[u][v] - (double)c[v];
+          a[v] += t;
+          b[v] = fma(t, t, b[v]);
+        }
+    }
+    for (; k < H; ++k) {
+      const fv x = *reinterpret_cast<const fv*>(col + k * rs);
+#pragma unroll
+      for (int v = 0; v < W; ++v) {
+        const double t = (double)x[v] - (double)c[v];
+        a[v] += t;
+        b[v] = fma(t, t, b[v]);
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < W; ++v) acc += b[v] - a[v] * a[v] / (double)H;
+  }
+  acc = block_sum(acc, scratch);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+__global__ void __launch_bounds__(256) honest_var_final(const double* __restrict__ part, int nb,
+                                                        int64_t H, float* __restrict__ out) {
+  __shared__ double scratch[16];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[i];
+  s = block_sum(s, scratch);
+  if (threadIdx.x == 0) out[0] = (float)(s / (double)H);
+}
+
+int honest_var_blocks(int64_t d, int num_cu) {
+  const int64_t g = (d / 4 + 255) / 256;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, 4 * (int64_t)num_cu));
+}
+
+hipError_t launch_honest_var(const float* X, int64_t H, int64_t d, int64_t ldx, int wshift,
+                             int nb, double* part, float* out, hipStream_t s) {
+  const bool v4 = d % 4 == 0 && (wshift ? true : ldx % 4 == 0) &&
+                  reinterpret_cast<uintptr_t>(X) % 16 == 0;
+  if (v4)
+    hipLaunchKernelGGL(honest_var_part<4>, dim3(nb), dim3(256), 0, s, X, H, d, ldx, wshift, part);
+  else
+    hipLaunchKernelGGL(honest_var_part<1>, dim3(nb), dim3(256), 0, s, X, H, d, ldx, wshift, part);
+  hipLaunchKernelGGL(honest_var_final, dim3(1), dim3(256), 0, s, part, nb, H, out);
+  return hipGetLastError();
+}
+
 // Order statistics by bit-wise selection on order-preserving keys.
 //
 // A column's K values live across one wave: lane l holds rows l, l+64, ...

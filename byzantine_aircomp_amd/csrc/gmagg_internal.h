@@ -148,6 +148,10 @@ hipError_t launch_col_mean(const float* X, int64_t K, int64_t d, int64_t ldx, fl
                            hipStream_t s);
 hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, int mode,
                              int64_t b, float* out, hipStream_t s);
+// getVarience (M:127-129): one streaming pass, part[nb] fp64 block partials.
+int honest_var_blocks(int64_t d, int num_cu);
+hipError_t launch_honest_var(const float* X, int64_t H, int64_t d, int64_t ldx, int wshift,
+                             int nb, double* part, float* out, hipStream_t s);
 // Krum: D [K][K] fp64, part [krum_slices(K, d)][K][K] fp64, score [K] fp64.
 int64_t krum_slices(int64_t K, int64_t d);
 hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t kk, double* D,
@@ -160,7 +164,7 @@ hipError_t launch_rows_to_panels(const float* X, int64_t K, int64_t d, int64_t l
                                  int64_t W, int64_t pstride, hipStream_t s);
 hipError_t launch_oma_philox(float* X, int64_t K, int64_t d, int64_t ldx, int64_t d_total,
                              int64_t col_off, float sd, uint64_t seed, hipStream_t s,
-                             int wshift = 0);
+                             int wshift = 0, int64_t problems = 1, int64_t pstride = 0);
 hipError_t launch_fill_clients(float* X, int64_t K, int64_t d, int64_t ldx, int64_t B,
                                float mu_h, float sd_h, float mu_b, float sd_b, int64_t d_total,
                                int64_t col_off, uint64_t seed, hipStream_t s);

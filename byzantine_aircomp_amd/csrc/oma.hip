@@ -47,10 +47,14 @@ __global__ void __launch_bounds__(256) oma_apply(float* __restrict__ X, int64_t 
 // ALIGNED: col_off % 4 == 0 (every unsharded call and the 256-aligned shards), so
 // a group of 4 columns is exactly one Philox block; otherwise (the shift is the same
 // for every group of the launch) a group spans two blocks.
+// Batched (BASELINE C5, the reference's `--agg gm2 --var v` pre-noise on P
+// independent problems): rows r = p * Kp + k of P problems [P][Kp] at X + p * pstride;
+// problem p is keyed with seed + p * kSeedStride (row k, as a single call would).
 template <bool ALIGNED, bool VEC4>
 __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t K, int64_t d,
                                                   int64_t ldx, int64_t col_off, float sd,
-                                                  uint64_t seed, int wshift) {
+                                                  uint64_t seed0, int wshift, int64_t Kp,
+                                                  int64_t pstride) {
   // x + scale*z rounds the same (no FMA) on the float4 and the scalar path, in
   // every instantiation: a shard or a layout must reproduce the others bit for bit
 #pragma clang fp contract(off)
@@ -61,12 +65,14 @@ __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t
   constexpr int U = GMK_OMA_U;                // groups per thread per step: U=4 17.4 ms vs U=2 17.7 at C3 size
   const int64_t G = (d + 3) / 4;
   const int64_t T = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t k = blockIdx.y; k < K; k += gridDim.y) {
+  for (int64_t r = blockIdx.y; r < K; r += gridDim.y) {
+    const int64_t pi = r / Kp, k = r - pi * Kp;
+    const uint64_t seed = seed0 + (uint64_t)pi * kSeedStride;
     float h[4];
     normal4_hw(seed, kStreamOmaChannel, 0, (uint64_t)k, h);
     const float a = h[0] * 0.70710678118654752f, b = h[1] * 0.70710678118654752f;
     const float scale = sd / sqrtf(a * a + b * b);
-    float* row = wshift ? X + (k << wshift) : X + k * ldx;
+    float* row = (wshift ? X + (k << wshift) : X + k * ldx) + pi * pstride;
     // Step s covers groups g0 + q*T (q < U).  Step s+1's loads are issued before
     // step s's Philox math and stores, so each thread keeps U loads in flight
     // across its whole loop (the draws do not depend on the data).
@@ -188,27 +194,30 @@ hipError_t launch_oma_apply(float* X, int64_t K, int64_t d, int64_t ldx, const f
 
 hipError_t launch_oma_philox(float* X, int64_t K, int64_t d, int64_t ldx, int64_t d_total,
                              int64_t col_off, float sd, uint64_t seed, hipStream_t s,
-                             int wshift) {
+                             int wshift, int64_t problems, int64_t pstride) {
   (void)d_total;   // draws are keyed by (row, global column quad): no d_total needed
+  const int64_t Kp = K;
+  K *= problems;   // rows of all problems
   const int64_t G = (d + 3) / 4;
   const int gy = (int)(K < 65535 ? K : 65535);
   int64_t gx = (G + 255) / 256;
   const int64_t cap = std::max<int64_t>(1, (8192 + gy - 1) / gy);   // ~8K blocks in flight
   if (gx > cap) gx = cap;
-  const int vec4 = (reinterpret_cast<uintptr_t>(X) % 16 == 0) && ldx % 4 == 0;
+  const int vec4 = (reinterpret_cast<uintptr_t>(X) % 16 == 0) && ldx % 4 == 0 &&
+                   (problems == 1 || pstride % 4 == 0);
   const dim3 grid((unsigned)gx, gy);
   if (col_off % 4 == 0 && vec4)
     hipLaunchKernelGGL((oma_philox<true, true>), grid, dim3(256), 0, s, X, K, d, ldx, col_off, sd,
-                       seed, wshift);
+                       seed, wshift, Kp, pstride);
   else if (col_off % 4 == 0)
     hipLaunchKernelGGL((oma_philox<true, false>), grid, dim3(256), 0, s, X, K, d, ldx, col_off, sd,
-                       seed, wshift);
+                       seed, wshift, Kp, pstride);
   else if (vec4)
     hipLaunchKernelGGL((oma_philox<false, true>), grid, dim3(256), 0, s, X, K, d, ldx, col_off, sd,
-                       seed, wshift);
+                       seed, wshift, Kp, pstride);
   else
     hipLaunchKernelGGL((oma_philox<false, false>), grid, dim3(256), 0, s, X, K, d, ldx, col_off, sd,
-                       seed, wshift);
+                       seed, wshift, Kp, pstride);
   return hipGetLastError();
 }
 

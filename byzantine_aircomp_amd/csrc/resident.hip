@@ -63,26 +63,28 @@ __device__ __forceinline__ void put_value(gu64* g, unsigned tag, double v) {
   __hip_atomic_store(g + 1, t | (u & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Sum over blocks b = 0..nb-1 (in that order) of value `col` of pass `tag`:
-// every granule pair is loaded at once (NB_CHUNK blocks per round trip), re-read
-// until all tags match.  The poll is bounded in WALL time (s_memrealtime): on
-// timeout (a time-sliced GPU, blocks not co-resident) the flag tmo is raised and
-// every block gives up; the host then reruns the problem on the streaming path.
-constexpr int kNbChunk = 8;
+// Sum over blocks b = g, g + G, g + 2G, ... (< nb, in that order) of one value of
+// pass `tag`: the granule pairs are loaded at once (kNbChunk blocks per round
+// trip) and re-read until every tag matches.  The poll is bounded in WALL time
+// (s_memrealtime): on timeout (a time-sliced GPU, blocks not co-resident) the
+// flag tmo is raised and every block gives up; the host then reruns the problem
+// on the streaming path.
+constexpr int kNbChunk = 4;
 
-__device__ __forceinline__ bool gather_value(const gu64* g, int64_t bstride, unsigned nb,
-                                             unsigned tag, gu32* tmo, double& sum) {
+__device__ __forceinline__ bool gather_value(const gu64* g, int64_t bstride, unsigned b_first,
+                                             unsigned b_step, unsigned nb, unsigned tag,
+                                             gu32* tmo, double& sum) {
   sum = 0.0;
-  for (unsigned b0 = 0; b0 < nb; b0 += kNbChunk) {
-    const int n = (int)(nb - b0 < (unsigned)kNbChunk ? nb - b0 : kNbChunk);
+  for (unsigned b0 = b_first; b0 < nb; b0 += kNbChunk * b_step) {
     unsigned long long hi[kNbChunk], lo[kNbChunk];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned spins = 0;; ++spins) {
       bool ok = true;
 #pragma unroll
       for (int j = 0; j < kNbChunk; ++j) {
-        if (j < n) {
-          const gu64* q = g + (int64_t)(b0 + j) * bstride;
+        const unsigned b = b0 + j * b_step;
+        if (b < nb) {
+          const gu64* q = g + (int64_t)b * bstride;
           hi[j] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           lo[j] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           ok &= (unsigned)(hi[j] >> 32) == tag && (unsigned)(lo[j] >> 32) == tag;
@@ -100,7 +102,7 @@ __device__ __forceinline__ bool gather_value(const gu64* g, int64_t bstride, uns
     }
 #pragma unroll
     for (int j = 0; j < kNbChunk; ++j)
-      if (j < n)
+      if (b0 + j * b_step < nb)
         sum += __longlong_as_double((long long)(((hi[j] & 0xffffffffull) << 32) |
                                                 (lo[j] & 0xffffffffull)));
   }
@@ -131,6 +133,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   __shared__ double s_r[KMAX];
   __shared__ double s_tot[2];
   __shared__ double s_wp[2 * NW];
+  __shared__ double s_part[NW * 64];
   __shared__ double scratch[16];
   __shared__ float s_anoise;
   __shared__ int s_ok;
@@ -232,24 +235,37 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
 #endif
   for (;; ++it) {
     // (1) gather pass `it` (INIT at it = 0): D2 (+ r at it = 0) and the per-wave
-    // movement / norm partials, summed over blocks in block order
+    // movement / norm partials.  G thread groups each sum every G-th block (in
+    // block order, one round trip of loads), then the G group sums are added in
+    // group order: a fixed order whatever the timing.
     {
       const gu64* in = gran + (it & 1) * nb * 2 * NV;
       const unsigned tag = (unsigned)(it + 1);
-      const int64_t nk = it == 0 ? 2 * K : K;
-      const int64_t ncol = nk + 2 * NW;
+      const int nk = (int)(it == 0 ? 2 * K : K);
+      const int ncol = nk + 2 * NW;
+      const int G = max(1, min((int)blockDim.x / ncol, (int)((nb + kNbChunk - 1) / kNbChunk)));
       bool ok = true;
-      for (int64_t cc = tid; cc < ncol; cc += blockDim.x) {
+      for (int t = tid; t < G * ncol; t += blockDim.x) {
+        const int g = t / ncol, cc = t - g * ncol;
         const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
         double sum;
-        if (!gather_value(in + 2 * v, 2 * NV, nb, tag, tmo, sum)) { ok = false; break; }
-        if (cc < K) s_d2[cc] = sum;
-        else if (cc < nk) s_r[cc - K] = sum;
-        else s_wp[cc - nk] = sum;
+        if (!gather_value(in + 2 * v, 2 * NV, (unsigned)g, (unsigned)G, nb, tag, tmo, sum)) {
+          ok = false;
+          break;
+        }
+        s_part[t] = sum;
       }
       if (!ok) s_ok = 0;
       __syncthreads();
       if (s_ok == 0) return;                       // timed out: every thread leaves
+      for (int cc = tid; cc < ncol; cc += blockDim.x) {
+        double sum = 0.0;
+        for (int g = 0; g < G; ++g) sum += s_part[g * ncol + cc];
+        if (cc < K) s_d2[cc] = sum;
+        else if (cc < nk) s_r[cc - K] = sum;
+        else s_wp[cc - nk] = sum;
+      }
+      __syncthreads();
       if (tid == 0) {
         double m = 0.0, g = 0.0;
         for (int ww = 0; ww < NW; ++ww) {
@@ -434,9 +450,10 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
 // ---------------------------------------------------------------------------
 
 // Chunks per block: CPB * J columns must map one finisher column per thread, and
-// the tile x[CPB][R][V] must stay within 64 VGPRs.
+// the tile x[CPB][R][V] must stay within 16 VGPRs (1024-thread blocks have 128
+// VGPRs; 32-register tiles spilled).
 constexpr bool res_cpb_ok(int V, int NW, int LPR, int R, int CPB) {
-  return CPB == 1 || (CPB * LPR * V <= NW * 64 && CPB * R * V <= 64);
+  return CPB == 1 || (CPB * LPR * V <= NW * 64 && CPB * R * V <= 16);
 }
 
 template <int V, int NW, int LPR, int R, int CPB>

@@ -183,10 +183,25 @@ int gm_trimmed_mean_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64
 int gm_krum_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t ldx,
                 int64_t honest_size, float* out, int64_t* index, void* stream);
 
+/* getVarience(w_local, honestSize) (MNIST_Air_weight.py:127-129): the mean over the
+ * first `honest` rows of ||x_k - mean||^2, written as ONE fp32 value to the device
+ * pointer `out`; one streaming pass over the honest rows (fp64 sums). */
+int gm_honest_variance_f32(gm_ctx* ctx, const float* X, int64_t honest, int64_t d, int64_t ldx,
+                           float* out, void* stream);
+/* The same on a client matrix of K rows in the panel layout (GM_LAYOUT_PANELS). */
+int gm_honest_variance_panels_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t honest,
+                                  int64_t d, int64_t panel_stride, float* out, void* stream);
+
 /* OMA(message, noise_var): in-place per-client equalised AWGN
  * (MNIST_Air_weight.py:385-394), draws from on-device Philox keyed by `seed`. */
 int gm_oma_philox_f32(gm_ctx* ctx, float* X, int64_t K, int64_t d, int64_t ldx,
                       double noise_var, uint64_t seed, void* stream);
+
+/* OMA on P independent problems X[p] = X + p*pstride ([K][ldx] each; BASELINE C5,
+ * the reference's `--agg gm2 --var v` pre-noise, MNIST_Air_weight.py:351-352):
+ * problem p's draws are gm_oma_philox_f32's with seed + p * 0x9E3779B97F4A7C15. */
+int gm_oma_philox_batched_f32(gm_ctx* ctx, float* X, int64_t P, int64_t K, int64_t d, int64_t ldx,
+                              int64_t pstride, double noise_var, uint64_t seed, void* stream);
 
 /* The same OMA on client updates in the panel layout (GM_LAYOUT_PANELS: X as
  * [ceil(d/W)][K][W], W = gm_panel_width(K), panel_stride >= K*W): identical draws

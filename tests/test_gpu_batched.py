@@ -56,3 +56,34 @@ def test_batched_mixed_convergence():
         want, tr = orc.gm2(X[i].clone(), {"maxiter": 1000, "tol": 1e-6, "guess": p[i].clone()})
         assert rel_l2(out[i].cpu().numpy(), want.numpy()) <= 1e-5
         assert abs(iters[i] - tr.iters) <= 1
+
+
+@pytest.mark.parametrize("P,K,d", [(5, 50, 10_000), (3, 7, 333)])
+def test_oma_batched_equals_single_calls(P, K, d):
+    """C5 in the reference's literal `--agg gm2 --var v` reading (M:351-353): the
+    batched OMA pre-noise of problem p is bit-identical to OMA(X[p]) with seed
+    + p * SEED_STRIDE (float4 path at d % 4 == 0, scalar path otherwise)."""
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd.batched import SEED_STRIDE, oma_batched
+    X, _ = _problems(P, K, d, seed=17)
+    X = X.cuda()
+    batched = oma_batched(X.clone(), 1e-2, seed=123)
+    for i in range(P):
+        single = X[i].clone()
+        bz.OMA(single, 1e-2, seed=(123 + i * SEED_STRIDE) % 2 ** 64)
+        assert torch.equal(batched[i], single), i
+    assert not torch.equal(batched, X)
+
+
+def test_c5_prenoise_reading_matches_oracle():
+    """OMA pre-noise then gm2, batched, vs the oracle gm2 on the same noisy problems."""
+    from byzantine_aircomp_amd.batched import gm2_batched, oma_batched
+    P, K, d = 4, 50, 8192
+    X, p = _problems(P, K, d, seed=23)
+    Xn = oma_batched(X.cuda(), 1e-3, seed=7)
+    out, res = gm2_batched(Xn, {"maxiter": 1000, "guess": p.cuda()})
+    Xh = Xn.cpu()
+    for i in range(P):
+        want, tr = orc.gm2(Xh[i].clone(), {"maxiter": 1000, "tol": 1e-5, "guess": p[i].clone()})
+        assert rel_l2(out[i].cpu().numpy(), want.numpy()) <= 1e-5
+        assert abs(res[i].iters - tr.iters) <= 1
