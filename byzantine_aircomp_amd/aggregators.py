@@ -46,7 +46,7 @@ from . import _lib
 from .panels import ClientPanels
 
 __all__ = ["gm2", "gm", "OMA", "mean", "median", "trimmed_mean", "Krum", "GMResult",
-           "last_result", "Context", "context"]
+           "last_result", "Context", "context", "honest_variance"]
 
 
 @dataclass
@@ -314,6 +314,32 @@ def Krum(wList, options):  # noqa: N802 - reference name (M:197)
                                        _stream_ptr(X.device)), "gm_krum_f32")
     Krum.last_index = idx.value
     return out if wList.device == out.device else out.to(wList.device)
+
+
+def honest_variance(w_local, honestSize: int) -> torch.Tensor:
+    """getVarience (M:127-129) on the device: the mean over the first honestSize rows
+    of ||x_k - mean||^2, one streaming pass (fp64 sums); a 0-dim fp32 tensor."""
+    out = torch.empty((), dtype=torch.float32, device=w_local.device)
+    if isinstance(w_local, ClientPanels):
+        ctx = context(w_local.device)
+        with torch.cuda.device(w_local.device):
+            _lib.check(ctx.lib.gm_honest_variance_panels_f32(
+                ctx.handle, w_local.data.data_ptr(), w_local.K, int(honestSize), w_local.d,
+                w_local.panel_stride, out.data_ptr(), _stream_ptr(w_local.device)),
+                "gm_honest_variance_panels_f32")
+        return out
+    if w_local.device.type != "cuda" or w_local.dtype != torch.float32 or w_local.dim() != 2:
+        raise TypeError("honest_variance needs an fp32 CUDA [K, d] matrix or ClientPanels")
+    X = w_local if (w_local.stride(1) == 1 and w_local.stride(0) >= w_local.shape[1]) \
+        else w_local.contiguous()
+    if not 1 <= honestSize <= X.shape[0]:
+        raise ValueError(f"honestSize {honestSize} not in [1, {X.shape[0]}]")
+    ctx = context(X.device)
+    with torch.cuda.device(X.device):
+        _lib.check(ctx.lib.gm_honest_variance_f32(
+            ctx.handle, X.data_ptr(), int(honestSize), X.shape[1], max(X.stride(0), X.shape[1]),
+            out.data_ptr(), _stream_ptr(X.device)), "gm_honest_variance_f32")
+    return out
 
 
 def OMA(message, noise_var=0.01, noise_source=None, seed=None):  # noqa: N802 - reference name

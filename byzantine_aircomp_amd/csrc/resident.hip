@@ -452,8 +452,11 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
 // Chunks per block: CPB * J columns must map one finisher column per thread, and
 // the tile x[CPB][R][V] must stay within 16 VGPRs (1024-thread blocks have 128
 // VGPRs; 32-register tiles spilled).
+#ifndef GMK_RES_TILE_REGS
+#define GMK_RES_TILE_REGS 16   // A/B knob: 32 allows 16 blocks at C2 (with spills)
+#endif
 constexpr bool res_cpb_ok(int V, int NW, int LPR, int R, int CPB) {
-  return CPB == 1 || (CPB * LPR * V <= NW * 64 && CPB * R * V <= 16);
+  return CPB == 1 || (CPB * LPR * V <= NW * 64 && CPB * R * V <= GMK_RES_TILE_REGS);
 }
 
 template <int V, int NW, int LPR, int R, int CPB>

@@ -96,7 +96,15 @@ def calculateAccuracy(model, loss_func, loader, device):  # noqa: N802 - M:106-1
     return loss_sum / total, correct / total
 
 
-def getVarience(w_local, honestSize):  # noqa: N802 - M:127-129 (one streaming pass)
+def getVarience(w_local, honestSize):  # noqa: N802 - M:127-129
+    """Mean over the honest rows of ||x_k - honest mean||^2.  On the device (a CUDA
+    fp32 [K, d] matrix or ClientPanels) it is ONE streaming pass of the HIP kernel
+    gm_honest_variance_f32 (fp64 sums); a CPU matrix (the reference loop's own
+    tensors) keeps the reference's torch expression."""
+    from .panels import ClientPanels
+    if isinstance(w_local, ClientPanels) or (w_local.is_cuda and w_local.dtype == torch.float32):
+        from .aggregators import honest_variance
+        return honest_variance(w_local, honestSize)
     h = w_local[:honestSize]
     return torch.mean(((h - h.mean(dim=0)) ** 2).sum(dim=1))
 
@@ -118,20 +126,37 @@ def weightflip(messages, byzantinesize):
 # ---- device-resident client packing (row f2) --------------------------------------
 
 class ClientUpdates:
-    """[K, d] matrix of client parameter vectors, resident on the model's device."""
+    """K client parameter vectors, resident on the model's device.
 
-    def __init__(self, model: nn.Module, K: int, device=None):
+    layout="rows": a [K, d] matrix (flatten_list's stack, M:206-209), row k written
+    in place.  layout="panels": a ClientPanels — the same values in the panel layout
+    the streaming pass reads contiguously (the C3 headline's input), client k
+    scattered into it by `store` (one kernel-free strided copy per client); gm / gm2
+    and OMA take it directly."""
+
+    def __init__(self, model: nn.Module, K: int, device=None, layout: str = "rows"):
         self.params = list(model.parameters())
         self.d = sum(p.numel() for p in self.params)
         dev = device if device is not None else self.params[0].device
-        self.X = torch.empty(K, self.d, dtype=torch.float32, device=dev)
+        if layout not in ("rows", "panels"):
+            raise ValueError(f"layout must be 'rows' or 'panels' (got {layout!r})")
+        self.layout = layout
+        if layout == "panels":
+            from .panels import ClientPanels
+            self.X = ClientPanels(K, self.d, device=dev)
+            self._buf = torch.empty(self.d, dtype=torch.float32, device=dev)
+        else:
+            self.X = torch.empty(K, self.d, dtype=torch.float32, device=dev)
 
     def flat(self, out=None):
         """The model's parameters as one vector (flatten_list's row layout)."""
         return torch.cat([p.detach().reshape(-1) for p in self.params], out=out)
 
     def store(self, k: int):
-        self.flat(out=self.X[k])
+        if self.layout == "panels":
+            self.X.store(k, self.flat(out=self._buf))
+        else:
+            self.flat(out=self.X[k])
 
     def load(self, vector: torch.Tensor):
         """Copy an aggregate back into the parameters (M:354-358) through views."""
@@ -154,8 +179,14 @@ def _log(*k):
 def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # noqa: N802
         byzantineSize=0, attack=None, rounds=10, displayInterval=1000, SEED=None,
         fixSeed=False, loss_func=None, train_dataset=None, validate_dataset=None, device=None,
-        batchSize=None, num_classes=10, verbose=True, **kw):
-    """Federated SGD with K = honest + Byzantine simulated clients (M:226-372)."""
+        batchSize=None, num_classes=10, verbose=True, layout="rows", eval_train=True, **kw):
+    """Federated SGD with K = honest + Byzantine simulated clients (M:226-372).
+    layout="panels" keeps the client matrix in the panel layout (gm / gm2 only).
+    EMNIST_Air_weight.py's variant: num_classes=62 (its MLP(784, 62) and 61 - y
+    relabel, E:101, E:321) and eval_train=False (train loss / accuracy recorded as
+    0, 0, E:273-274, E:364-365)."""
+    def train_eval():
+        return calculateAccuracy(model, loss_func, train_all, device) if eval_train else (0, 0)
     assert byzantineSize == 0 or attack is not None
     assert honestSize != 0
     if fixSeed:
@@ -176,15 +207,18 @@ def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # 
     streams = [iter(DL(dataset=shards[i], batch_size=batchSize, sampler=samplers[i]))
                for i in range(K)]
 
-    tl, ta = calculateAccuracy(model, loss_func, train_all, device)
+    tl, ta = train_eval()
     vl, va = calculateAccuracy(model, loss_func, val_all, device)
     paths = {"train_loss": [tl], "train_acc": [ta], "val_loss": [vl], "val_acc": [va], "var": []}
     if verbose:
         _log(f"[0/{rounds}] train: loss={tl:.4f} acc={ta:.4f} val: loss={vl:.4f} acc={va:.4f}")
 
-    clients = ClientUpdates(model, K)
-    params = clients.params
     attack_name = attack.__name__ if attack is not None else None
+    if layout == "panels" and (aggregate.__name__ not in ("gm", "gm2") or attack_name == "weightflip"):
+        raise ValueError("layout='panels' supports the gm / gm2 aggregators and the classflip / "
+                         "dataflip attacks (weightflip and the coordinate-wise aggregators need rows)")
+    clients = ClientUpdates(model, K, layout=layout)
+    params = clients.params
     is_gm = aggregate.__name__ == "gm"
     if noise_var is not None and not is_gm:
         from .aggregators import OMA
@@ -213,7 +247,7 @@ def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # 
                 OMA(X, noise_var)                         # M:351-352
             clients.load(aggregate(X, options))           # M:353-358
         paths["var"].append(getVarience(clients.X, honestSize).cpu())
-        tl, ta = calculateAccuracy(model, loss_func, train_all, device)
+        tl, ta = train_eval()
         vl, va = calculateAccuracy(model, loss_func, val_all, device)
         for key, v in (("train_loss", tl), ("train_acc", ta), ("val_loss", vl), ("val_acc", va)):
             paths[key].append(v)

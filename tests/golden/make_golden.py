@@ -34,17 +34,18 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference/MNIST_Air_weight.py"
+REF_EMNIST = "/root/reference/EMNIST_Air_weight.py"
 sys.path.insert(0, ROOT)
 
 from oracle import aggregators as orc  # noqa: E402
 
 
-def load_reference():
+def load_reference(path=REF, name="byz_reference"):
     sys.dont_write_bytecode = True      # the reference tree is read-only
-    for name in ("torchvision", "torchvision.transforms"):
-        sys.modules.setdefault(name, types.ModuleType(name))
+    for mod_name in ("torchvision", "torchvision.transforms"):
+        sys.modules.setdefault(mod_name, types.ModuleType(mod_name))
     sys.modules["torchvision"].transforms = sys.modules["torchvision.transforms"]
-    spec = importlib.util.spec_from_file_location("byz_reference", REF)
+    spec = importlib.util.spec_from_file_location(name, path)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     return mod
@@ -273,5 +274,56 @@ def e2e(ref, manifest, save):
             weights=w)
 
 
+def synthetic_emnist(seed, n, classes=62):
+    proto = np.random.default_rng(700).standard_normal((classes, 1, 28, 28)).astype(np.float32)
+    r = np.random.default_rng(seed)
+    y = r.integers(0, classes, n).astype(np.int64)
+    x = (proto[y] + 2.0 * r.standard_normal((n, 1, 28, 28))).astype(np.float32)
+    return x, y
+
+
+def e2e_emnist():
+    """EMNIST_Air_weight.py's SGD (its MLP(784, 62): d = 48,670; the classflip
+    relabel 61 - y, E:321; no train-set evaluation, E:273-274 / E:364-365) on a
+    synthetic 62-class EMNIST-shaped set; appended to golden.json
+    (`python tests/golden/make_golden.py --emnist`)."""
+    ref = load_reference(REF_EMNIST, "byz_reference_emnist")
+    torch.set_num_threads(8)
+    path = os.path.join(HERE, "golden.json")
+    manifest = json.load(open(path))
+    manifest["cases"] = [c for c in manifest["cases"] if not c["name"].startswith("e2e_emnist")]
+    ce = torch.nn.CrossEntropyLoss()
+    loss = lambda o, t: ce(o, t.long())  # noqa: E731  (61.0 - targets is a float, E:321)
+    xtr, ytr = synthetic_emnist(701, 2000)
+    xva, yva = synthetic_emnist(702, 500)
+    for agg, var in (("gm2", None), ("gm", 1e-2)):
+        tr = torch.utils.data.TensorDataset(torch.from_numpy(xtr), torch.from_numpy(ytr))
+        va = torch.utils.data.TensorDataset(torch.from_numpy(xva), torch.from_numpy(yva))
+        model = ref.modelFactory(SEED=2021)
+        res = ref.SGD(model, gamma=1e-2, aggregate=getattr(ref, agg), weight_decay=0.0,
+                      noise_var=var, honestSize=45, byzantineSize=5,
+                      attack=ref.classflip, rounds=2, displayInterval=2, SEED=2021,
+                      fixSeed=True, loss_func=loss, train_dataset=tr,
+                      validate_dataset=va, device=torch.device("cpu"), batchSize=50)
+        m, tl, ta, vl, va_, vp = res
+        w = torch.cat([p.detach().flatten() for p in m.parameters()]).numpy()
+        name = f"e2e_emnist_classflip_{agg}"
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), weights=w)
+        manifest["cases"].append({
+            "func": "SGD", "reference": "EMNIST_Air_weight.py", "aggregate": agg,
+            "noise_var": var, "K": 50, "B": 5, "num_classes": 62, "d": int(w.size),
+            "rounds": 2, "displayInterval": 2, "SEED": 2021, "batchSize": 50,
+            "gamma": 1e-2, "data_seeds": [701, 702], "n_train": 2000, "n_val": 500,
+            "trainLossPath": tl, "trainAccPath": ta, "valLossPath": vl,
+            "valAccPath": va_, "variencePath": [float(v) for v in vp],
+            "name": name, "file": name + ".npz"})
+    with open(path, "w") as f:
+        json.dump(manifest, f, indent=1)
+    print("wrote EMNIST e2e cases")
+
+
 if __name__ == "__main__":
-    main()
+    if "--emnist" in sys.argv:
+        e2e_emnist()
+    else:
+        main()

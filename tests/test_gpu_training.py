@@ -19,7 +19,7 @@ def synthetic_mnist(seed, n):
     return torch.from_numpy(x), torch.from_numpy(y)
 
 
-def _run(agg_name, device, monkeypatch):
+def _run(agg_name, device, monkeypatch, layout="rows"):
     import byzantine_aircomp_amd as bz
     from byzantine_aircomp_amd import training as T
     meta, arr = golden_case(f"e2e_sgd_classflip_{agg_name}")
@@ -33,7 +33,7 @@ def _run(agg_name, device, monkeypatch):
                 honestSize=45, byzantineSize=5, attack=T.classflip, rounds=2, displayInterval=2,
                 SEED=2021, fixSeed=True, loss_func=torch.nn.CrossEntropyLoss(),
                 train_dataset=tr, validate_dataset=va, device=torch.device(device),
-                batchSize=50, verbose=False)
+                batchSize=50, verbose=False, layout=layout)
     m, tl, ta, vl, vacc, var = res
     w = torch.cat([p.detach().flatten().cpu() for p in m.parameters()]).numpy()
     return meta, arr, w, tl, ta, vl, vacc, var
@@ -59,6 +59,31 @@ def test_loop_device_resident_matches_reference(agg_name, monkeypatch):
     np.testing.assert_allclose(vl, meta["valLossPath"], rtol=1e-4)
 
 
+@pytest.mark.parametrize("agg_name", ["gm2", "gm"])
+def test_loop_device_resident_panels_matches_reference(agg_name, monkeypatch):
+    """The same loop with the client matrix kept in the panel layout (the layout the
+    C3 headline streams): stores scatter into panels, OMA / gm / gm2 / getVarience
+    read them directly."""
+    meta, arr, w, tl, ta, vl, vacc, var = _run(agg_name, "cuda", monkeypatch, layout="panels")
+    assert rel_l2(w, arr["weights"]) <= 1e-4
+    np.testing.assert_allclose(tl, meta["trainLossPath"], rtol=1e-4)
+    np.testing.assert_allclose(vl, meta["valLossPath"], rtol=1e-4)
+    np.testing.assert_allclose([float(v) for v in var], meta["variencePath"], rtol=1e-4)
+
+
+def test_client_updates_panels_equal_rows():
+    from byzantine_aircomp_amd import training as T
+    m = T.MLP(784, 10).cuda()
+    rows, pan = T.ClientUpdates(m, 5), T.ClientUpdates(m, 5, layout="panels")
+    for k in range(5):
+        with torch.no_grad():
+            for p in m.parameters():
+                p.add_(0.5 * k)
+        rows.store(k)
+        pan.store(k)
+    assert torch.equal(pan.X.to_rows(), rows.X)
+
+
 def test_client_updates_layout_is_flatten_list():
     from byzantine_aircomp_amd import training as T
     m = T.MLP(784, 10).cuda()
@@ -73,3 +98,30 @@ def test_client_updates_layout_is_flatten_list():
     assert cu.X.shape == (3, 7850) and cu.X.device.type == "cuda"
     cu.load(torch.zeros(7850, device="cuda"))
     assert all(float(p.abs().sum()) == 0 for p in m.parameters())
+
+
+@pytest.mark.parametrize("agg_name", ["gm2", "gm"])
+@pytest.mark.parametrize("layout", ["rows", "panels"])
+def test_emnist_loop_device_resident_matches_reference(agg_name, layout, monkeypatch):
+    """EMNIST_Air_weight.py's loop (62 classes, d = 48,670, 61 - y, no train-set
+    evaluation) with model, client matrix and aggregation on the GPU."""
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd import training as T
+    from test_training_cpu import synthetic_emnist
+    meta, arr = golden_case(f"e2e_emnist_classflip_{agg_name}")
+    if agg_name == "gm":
+        monkeypatch.setenv("BYZ_AIRCOMP_NOISE", "host")   # replay the reference's draws
+    tr = torch.utils.data.TensorDataset(*synthetic_emnist(701, 2000))
+    va = torch.utils.data.TensorDataset(*synthetic_emnist(702, 500))
+    model = T.modelFactory(SEED=2021, num_classes=62).cuda()
+    res = T.SGD(model, gamma=1e-2, aggregate=getattr(bz, agg_name), weight_decay=0.0,
+                noise_var=meta["noise_var"], honestSize=45, byzantineSize=5, attack=T.classflip,
+                rounds=2, displayInterval=2, SEED=2021, fixSeed=True,
+                loss_func=torch.nn.CrossEntropyLoss(), train_dataset=tr, validate_dataset=va,
+                device=torch.device("cuda"), batchSize=50, verbose=False, num_classes=62,
+                eval_train=False, layout=layout)
+    m, tl, ta, vl, vacc, var = res
+    w = torch.cat([p.detach().flatten() for p in m.parameters()]).cpu().numpy()
+    assert rel_l2(w, arr["weights"]) <= 1e-4
+    np.testing.assert_allclose(vl, meta["valLossPath"], rtol=1e-4)
+    np.testing.assert_allclose([float(v) for v in var], meta["variencePath"], rtol=1e-4)

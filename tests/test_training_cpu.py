@@ -42,6 +42,39 @@ def test_sgd_counterpart_bit_exact_with_reference(agg_name):
     assert [float(v) for v in var] == meta["variencePath"]
 
 
+def synthetic_emnist(seed, n, classes=62):
+    # same recipe as tests/golden/make_golden.py (synthetic_emnist)
+    proto = np.random.default_rng(700).standard_normal((classes, 1, 28, 28)).astype(np.float32)
+    r = np.random.default_rng(seed)
+    y = r.integers(0, classes, n).astype(np.int64)
+    x = (proto[y] + 2.0 * r.standard_normal((n, 1, 28, 28))).astype(np.float32)
+    return torch.from_numpy(x), torch.from_numpy(y)
+
+
+@pytest.mark.parametrize("agg_name", ["gm2", "gm"])
+def test_sgd_counterpart_bit_exact_with_emnist_reference(agg_name):
+    """EMNIST_Air_weight.py's loop: 62 classes (d = 48,670), the 61 - y flip
+    (E:321) and no train-set evaluation (E:273-274, E:364-365)."""
+    from byzantine_aircomp_amd import training as T
+    meta, arr = golden_case(f"e2e_emnist_classflip_{agg_name}")
+    tr = torch.utils.data.TensorDataset(*synthetic_emnist(701, 2000))
+    va = torch.utils.data.TensorDataset(*synthetic_emnist(702, 500))
+    model = T.modelFactory(SEED=2021, num_classes=62)
+    res = T.SGD(model, gamma=1e-2, aggregate=_as_aggregator(agg_name), weight_decay=0.0,
+                noise_var=meta["noise_var"], honestSize=45, byzantineSize=5,
+                attack=T.classflip, rounds=2, displayInterval=2, SEED=2021, fixSeed=True,
+                loss_func=torch.nn.CrossEntropyLoss(), train_dataset=tr, validate_dataset=va,
+                device=torch.device("cpu"), batchSize=50, verbose=False, num_classes=62,
+                eval_train=False)
+    m, tl, ta, vl, vacc, var = res
+    w = torch.cat([p.detach().flatten() for p in m.parameters()]).numpy()
+    assert w.size == meta["d"] == 48_670
+    assert np.array_equal(w, arr["weights"])
+    assert tl == meta["trainLossPath"] == [0, 0, 0] and ta == meta["trainAccPath"]
+    assert vl == meta["valLossPath"] and vacc == meta["valAccPath"]
+    assert [float(v) for v in var] == meta["variencePath"]
+
+
 def test_weightflip_on_device_matrix_semantics():
     from byzantine_aircomp_amd import training as T
     g = torch.Generator().manual_seed(3)
