@@ -109,7 +109,7 @@ struct ResArgs {
   int mode, has_noise;
   double P_max, noise_sd;
   uint64_t seed;
-  unsigned long long* gran;  // [2][gridDim.x][2 (2K + 2 NW)] {tag, half} granules (zeroed per call)
+  unsigned long long* gran;  // [2][gridDim.x][2K + 2] {tag, fp32} granules (zeroed per call)
   unsigned* bar;         // [2] timeout flag (zeroed per call)
   KState* st;
 };

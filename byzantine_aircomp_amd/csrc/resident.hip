@@ -33,6 +33,9 @@
 #ifndef GMK_RES_SLEEP
 #define GMK_RES_SLEEP 1   // spin back-off of the granule polls (A/B knob)
 #endif
+#ifndef GMK_RES_POLL1
+#define GMK_RES_POLL1 0   // poll one granule per chunk before reading the chunk (A/B knob; 0 was faster)
+#endif
 
 // -DGMK_RES_PROF: block 0 / thread 0 accumulates s_memrealtime (100 MHz) deltas per
 // phase of the iteration and prints them at the end (timing probe builds only).
@@ -56,11 +59,13 @@ constexpr uint64_t kPollTicks = 200000000ull;   // 2 s at the 100 MHz real-time 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 
-__device__ __forceinline__ void put_value(gu64* g, unsigned tag, double v) {
-  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
-  const unsigned long long t = (unsigned long long)tag << 32;
-  __hip_atomic_store(g, t | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(g + 1, t | (u & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// One partial = ONE 8-byte granule {tag, fp32 value}: a block's partial is an fp64
+// sum rounded once to fp32 (relative 6e-8; the reference's own norms are fp32
+// sums, M:174/M:180), the sum over blocks is fp64.  Half the granules of an fp64
+// {hi, lo} pair: the poll traffic on those lines is what the exchange costs.
+__device__ __forceinline__ void put_value(gu64* g, unsigned tag, float v) {
+  __hip_atomic_store(g, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Sum over blocks b = g, g + G, g + 2G, ... (< nb, in that order) of one value of
@@ -76,9 +81,25 @@ __device__ __forceinline__ bool gather_value(const gu64* g, int64_t bstride, uns
                                              gu32* tmo, double& sum) {
   sum = 0.0;
   for (unsigned b0 = b_first; b0 < nb; b0 += kNbChunk * b_step) {
-    unsigned long long hi[kNbChunk], lo[kNbChunk];
+    unsigned long long hi[kNbChunk];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned spins = 0;; ++spins) {
+      // wait on ONE granule of the chunk first: every thread of every block polls,
+      // and re-reading the whole chunk per round multiplied the uncached poll
+      // traffic on the few lines that hold the granules
+#if GMK_RES_POLL1
+      for (unsigned s1 = 0;; ++s1) {
+        const unsigned long long h0 = __hip_atomic_load(g + (int64_t)b0 * bstride, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)(h0 >> 32) == tag) break;
+        __builtin_amdgcn_s_sleep(GMK_RES_SLEEP > 0 ? GMK_RES_SLEEP : 1);
+        if ((s1 & 255u) == 255u && (__builtin_amdgcn_s_memrealtime() - t0 > kPollTicks ||
+                                    __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return false;
+        }
+      }
+#endif
       bool ok = true;
 #pragma unroll
       for (int j = 0; j < kNbChunk; ++j) {
@@ -86,8 +107,7 @@ __device__ __forceinline__ bool gather_value(const gu64* g, int64_t bstride, uns
         if (b < nb) {
           const gu64* q = g + (int64_t)b * bstride;
           hi[j] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          lo[j] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok &= (unsigned)(hi[j] >> 32) == tag && (unsigned)(lo[j] >> 32) == tag;
+          ok &= (unsigned)(hi[j] >> 32) == tag;
         }
       }
       if (ok) break;
@@ -103,17 +123,16 @@ __device__ __forceinline__ bool gather_value(const gu64* g, int64_t bstride, uns
 #pragma unroll
     for (int j = 0; j < kNbChunk; ++j)
       if (b0 + j * b_step < nb)
-        sum += __longlong_as_double((long long)(((hi[j] & 0xffffffffull) << 32) |
-                                                (lo[j] & 0xffffffffull)));
+        sum += (double)__uint_as_float((unsigned)(hi[j] & 0xffffffffull));
   }
   return true;
 }
 
-// Granule slots of one block and pass: value v at [2v, 2v+1];
-//   v < K: D2_k; K <= v < 2K: ||x_k||^2 (INIT); 2K + 2w, 2K + 2w + 1: wave w's
-//   movement and ||g||^2 partials.
+// Granule slots of one block and pass: value v at slot v;
+//   v < K: D2_k; K <= v < 2K: ||x_k||^2 (INIT); 2K, 2K + 1: the block's movement
+//   and ||g||^2 partials (summed over its waves in wave order).
 template <int NW>
-__host__ __device__ constexpr int64_t res_values(int64_t K) { return 2 * K + 2 * NW; }
+__host__ __device__ constexpr int64_t res_values(int64_t K) { return 2 * K + 2; }
 
 template <int V, int NW, int LPR, int R, int CPB>
 __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
@@ -132,7 +151,10 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   __shared__ double s_d2[KMAX];
   __shared__ double s_r[KMAX];
   __shared__ double s_tot[2];
-  __shared__ double s_wp[2 * NW];
+  __shared__ double s_wp[2];
+  __shared__ float s_h2[KMAX];
+  __shared__ float s_nd;
+  __shared__ double s_fin[2][NW];
   __shared__ double s_part[NW * 64];
   __shared__ double scratch[16];
   __shared__ float s_anoise;
@@ -170,23 +192,42 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   const int i_c = row_of_lane<LPR, R>(c);
   // publish this block's partials of pass p (granules, tag p + 1, buffer p & 1)
   auto publish = [&](int64_t p, const double* racc, const double* racc2, double mv, double gn) {
-    gu64* out = gran + ((p & 1) * nb + blockIdx.x) * 2 * NV;
+    gu64* out = gran + ((p & 1) * nb + blockIdx.x) * NV;
     const unsigned tag = (unsigned)(p + 1);
     if ((c % SPAN) == 0) {
 #pragma unroll
       for (int m = 0; m < RPL; ++m) {
         const int64_t k = rg + (int64_t)NRG * (i_c + m);
         if (k < K) {
-          put_value(out + 2 * k, tag, racc[m]);
-          if (racc2) put_value(out + 2 * (K + k), tag, racc2[m]);
+          put_value(out + k, tag, (float)racc[m]);
+          if (racc2) put_value(out + K + k, tag, (float)racc2[m]);
         }
       }
     }
-    mv = wave_sum(mv);
-    gn = wave_sum(gn);
+    if (tid == 0) {                 // s_fin: the waves' partials, published before a barrier
+      double m = 0.0, g = 0.0;
+      for (int ww = 0; ww < NW; ++ww) {
+        m += s_fin[0][ww];
+        g += s_fin[1][ww];
+      }
+      put_value(out + 2 * K, tag, (float)m);
+      put_value(out + 2 * K + 1, tag, (float)g);
+    }
+  };
+  // wave partials of the movement and ||g||^2 -> s_fin (read by publish after a
+  // barrier): fp32 sums over the finisher lanes (as the reference's fp32 norms),
+  // only in the waves that hold finisher columns
+  auto wave_partials = [&](float mv, float gn) {
+    if (w * 64 < JB) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        mv += __shfl_xor(mv, o, 64);
+        gn += __shfl_xor(gn, o, 64);
+      }
+    }
     if (lane == 0) {
-      put_value(out + 2 * (2 * K + 2 * w), tag, mv);
-      put_value(out + 2 * (2 * K + 2 * w + 1), tag, gn);
+      s_fin[0][w] = w * 64 < JB ? (double)mv : 0.0;
+      s_fin[1][w] = w * 64 < JB ? (double)gn : 0.0;
     }
   };
 
@@ -223,7 +264,9 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         racc2[m] += (double)e2[m];
       }
     }
-    publish(0, racc, racc2, 0.0, fin ? (double)(gcur * gcur) : 0.0);
+    wave_partials(0.f, fin ? gcur * gcur : 0.f);
+    __syncthreads();
+    publish(0, racc, racc2, 0.0, 0.0);
   }
 
   int64_t it = 0;
@@ -233,23 +276,37 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   uint64_t prof_[6] = {0, 0, 0, 0, 0, 0};
   uint64_t prev_ = __builtin_amdgcn_s_memrealtime();
 #endif
+  bool pre_h2 = false;
   for (;; ++it) {
     // (1) gather pass `it` (INIT at it = 0): D2 (+ r at it = 0) and the per-wave
     // movement / norm partials.  G thread groups each sum every G-th block (in
     // block order, one round trip of loads), then the G group sums are added in
     // group order: a fixed order whatever the timing.
     {
-      const gu64* in = gran + (it & 1) * nb * 2 * NV;
+      const gu64* in = gran + (it & 1) * nb * NV;
       const unsigned tag = (unsigned)(it + 1);
       const int nk = (int)(it == 0 ? 2 * K : K);
-      const int ncol = nk + 2 * NW;
+      const int ncol = nk + 2;
       const int G = max(1, min((int)blockDim.x / ncol, (int)((nb + kNbChunk - 1) / kNbChunk)));
+      // the K-space step's channel draws do not depend on the data: an idle wave
+      // draws them while the others gather
+      pre_h2 = a.mode == 1 && K <= 64 && G * ncol <= (NW - 1) * 64;
+      if (pre_h2 && w == NW - 1) {
+        if (lane < K) {
+          float n4[4];
+          normal4(a.seed, kStreamChannel, (uint64_t)it, (uint64_t)lane, n4);
+          const float hr = n4[0] * 0.70710678118654752f, hi = n4[1] * 0.70710678118654752f;
+          s_h2[lane] = hr * hr + hi * hi;                            // M:403
+        }
+        if (lane == 0)
+          s_nd = a.has_noise ? normal1(a.seed, kStreamNoise, (uint64_t)it, (uint64_t)d) : 0.f;
+      }
       bool ok = true;
       for (int t = tid; t < G * ncol; t += blockDim.x) {
         const int g = t / ncol, cc = t - g * ncol;
         const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
         double sum;
-        if (!gather_value(in + 2 * v, 2 * NV, (unsigned)g, (unsigned)G, nb, tag, tmo, sum)) {
+        if (!gather_value(in + v, NV, (unsigned)g, (unsigned)G, nb, tag, tmo, sum)) {
           ok = false;
           break;
         }
@@ -267,13 +324,8 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
       }
       __syncthreads();
       if (tid == 0) {
-        double m = 0.0, g = 0.0;
-        for (int ww = 0; ww < NW; ++ww) {
-          m += s_wp[2 * ww];
-          g += s_wp[2 * ww + 1];
-        }
-        s_tot[0] = m;
-        s_tot[1] = g;
+        s_tot[0] = s_wp[0];
+        s_tot[1] = s_wp[1];
       }
       __syncthreads();
     }
@@ -302,10 +354,15 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
           const double s2 = (double)s * (double)s;
           double ck = 0.0;
           if (kv) {
-            float n4[4];
-            normal4(a.seed, kStreamChannel, (uint64_t)it, (uint64_t)k, n4);
-            const float hr = n4[0] * 0.70710678118654752f, hi = n4[1] * 0.70710678118654752f;
-            const float h2 = hr * hr + hi * hi;                       // M:403
+            float h2;
+            if (pre_h2) {
+              h2 = s_h2[k];
+            } else {
+              float n4[4];
+              normal4(a.seed, kStreamChannel, (uint64_t)it, (uint64_t)k, n4);
+              const float hr = n4[0] * 0.70710678118654752f, hi = n4[1] * 0.70710678118654752f;
+              h2 = hr * hr + hi * hi;                                 // M:403
+            }
             const float dist = clamp_dist(s_d2[k], a.eps);
             const double dd = (double)dist;
             const double pk = (s_r[k] + s2) / (dd * dd * (double)(d + 1)) / (double)h2;   // M:404
@@ -313,9 +370,10 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
             ck = sqrt(a.P_max / pup) / dd;                            // M:407
           }
           const double Sc = wave_sum(ck);
-          const double nd = a.has_noise ? a.noise_sd * (double)normal1(a.seed, kStreamNoise,
-                                                                       (uint64_t)it, (uint64_t)d)
-                                        : 0.0;
+          const double nd = !a.has_noise ? 0.0
+                            : a.noise_sd * (double)(pre_h2 ? s_nd
+                                                           : normal1(a.seed, kStreamNoise,
+                                                                     (uint64_t)it, (uint64_t)d));
           const double scale = (double)s / ((double)s * Sc + nd);     // M:153-155
           if (kv) s_coef[k] = (float)(ck * scale);
           if (lane == 0) s_anoise = a.has_noise ? (float)(scale * a.noise_sd) : 0.f;
@@ -384,7 +442,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
       }
     }
     __syncthreads();
-    double mvp = 0.0, gnp = 0.0;
+    float mvp = 0.f, gnp = 0.f;
     if (tid < JB) {
       float gnew = 0.f;
       if (fin) {
@@ -395,12 +453,13 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         if (a.has_noise && a.mode == 1)
           gnew = fmaf(s_anoise, normal1(a.seed, kStreamNoise, (uint64_t)it, (uint64_t)gj), gnew);
         const float diff = gcur - gnew;
-        mvp = (double)(diff * diff);
-        gnp = (double)(gnew * gnew);
+        mvp = diff * diff;
+        gnp = gnew * gnew;
         gcur = gnew;
       }
       s_g[tid] = gnew;
     }
+    wave_partials(mvp, gnp);
     __syncthreads();
     RES_T(2)
     // (5) phase B: distances to the new iterate, every chunk, fp64 across chunks
@@ -518,7 +577,8 @@ bool resident_plan(const PassCfg& cfg, int64_t nch, int num_cu, int* cpb_out, in
 }
 
 size_t resident_gran_words(int64_t K, const PassCfg& cfg, int nb) {
-  return (size_t)2 * nb * 2 * (size_t)(2 * K + 2 * cfg.NW);
+  (void)cfg;
+  return (size_t)2 * nb * (size_t)(2 * K + 2);
 }
 
 hipError_t launch_resident(const PassCfg& cfg, int cpb, int grid, const ResArgs& a, hipStream_t s) {
