@@ -434,7 +434,8 @@ def main():
             return bz.aggregators.last_result
     layout = args.layout
     if layout == "auto":
-        layout = "panels" if args.workload.startswith("c3") and args.algo in ("auto", "stream") \
+        layout = "panels" if (args.workload.startswith("c3") and args.algo in ("auto", "stream")) \
+            or (args.workload.startswith("c4") and args.algo in ("auto", "stream", "gram")) \
             else "rows"
     panels = None
 
@@ -478,7 +479,7 @@ def main():
     alt = None
     alt_layout = "rows" if layout == "panels" else "panels"
     alt_steps = args.alt_steps if args.alt_steps is not None else max(3, args.steps // 4)
-    if alt_steps > 0 and (alt_layout == "rows" or (args.algo in ("auto", "stream")
+    if alt_steps > 0 and (alt_layout == "rows" or (args.algo in ("auto", "stream", "gram")
                                                    and bz.panel_width(K) > 0
                                                    and d_total >= 1 << 20)):
         a_el, a_ms, a_n, a_res, _ = measure(inputs(alt_layout), alt_steps, 1)

@@ -323,22 +323,30 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
 // loop.  Otherwise *rejected is set and the caller runs the streaming path.
 int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const float* guess0,
              float* out, const gm_opts* o, gm_result* res, const PassCfg& cfg, hipStream_t s,
-             bool split, bool guarded, bool* rejected) {
+             bool split, bool guarded, bool* rejected, int64_t pstride = 0) {
   *rejected = false;
+  // panels (pstride > 0): X is [ceil(d/W)][K][W] with W = the STEP tile's chunk width
+  // (cfg), a multiple of the Gram kernel's 64-column stage; the f16 kernel only
+  int wshift = 0;
+  if (pstride) {
+    const int W = cfg.LPR * cfg.V;
+    while ((1 << wshift) < W) ++wshift;
+    if ((1 << wshift) != W || W % 64 || !split) return fail(GM_ERR_UNSUPPORTED, "Gram on panels: W=%d", W);
+  }
   const int KT = gram_kt(K), KP = 32 * KT;
   // split: the scaled f16 kernel (3 products), rerun as the bf16 split (4 products,
   // the full fp32 exponent range) if its G came out non-finite (GMAGG_GRAM_KIND=bf16
   // forces the bf16 kernel: A/B)
   const char* kind_env = getenv("GMAGG_GRAM_KIND");
   const bool force_bf16 = kind_env && strcmp(kind_env, "bf16") == 0;
-  GramKind kind = !split ? GramKind::F32 : force_bf16 ? GramKind::BF16 : GramKind::H16;
+  GramKind kind = !split ? GramKind::F32 : (force_bf16 && !pstride) ? GramKind::BF16 : GramKind::H16;
   GramGrid gg = gram_grid(d, kind, c->num_cu);
   const GramGrid gb = gram_grid(d, GramKind::BF16, c->num_cu);
   const size_t slab_n = std::max(gram_slab_floats(KT, gg),
                                  kind == GramKind::H16 ? gram_slab_floats(KT, gb) : 0);
   // closing pass: the STEP tile when it also yields the distances (guarded), else
   // the lighter sum-only tile
-  const PassCfg ccfg = guarded ? cfg : light_cfg(K, cfg);
+  const PassCfg ccfg = (guarded || pstride) ? cfg : light_cfg(K, cfg);
   const int J = ccfg.LPR * ccfg.V;
   const int nb_p = (int)std::max<int64_t>(
       1, std::min<int64_t>((d + J - 1) / J,
@@ -358,7 +366,7 @@ again:
   hipEvent_t e0, e1;
   rc = record_pass_begin(c, s, &e0, &e1);
   if (rc) return rc;
-  HIPCHK(launch_gram(X, K, d, ldx, p, kind, gg, w.gslab, w.G, w.st, s));
+  HIPCHK(launch_gram(X, K, d, ldx, p, kind, gg, w.gslab, w.G, w.st, s, pstride, wshift));
   rc = record_pass_end(c, s, e0, e1);
   if (rc) return rc;
   rc = allreduce(c, w.G, (int64_t)KP * KP, s);
@@ -371,9 +379,10 @@ again:
   // closing pass: g = sum_k a_k x_k (+ the exact distances to g when guarded)
   const int64_t S = guarded ? K + 2 : 2;
   PassArgs a{};
-  a.X = X; a.K = K; a.d = d; a.ldx = ldx;
+  a.X = X; a.K = K; a.d = d; a.ldx = pstride ? pstride : ldx;
   a.g_old = p; a.g_new = out; a.coef = w.coef; a.st = w.st;
   a.slab = w.slab; a.slab_stride = S;
+  a.panel_stride = pstride;
   HIPCHK(launch_pass(ccfg, guarded ? 0 : 3, nb_p, a, s));
   HIPCHK(launch_slab_reduce(w.slab, nb_p, S, w.sums, w.st, s));   // [D (K)] [||p-g||^2, ||g||^2]
   rc = allreduce(c, w.sums, S, s);
@@ -384,6 +393,10 @@ again:
   HIPCHK(hipMemcpyAsync(hsums, w.sums + (S - 2), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (hst->gram_bad && kind == GramKind::H16) {   // rare: the f16 range was exceeded
+    if (pstride) {                                 // no bf16 panel kernel: streaming path
+      *rejected = true;
+      return GM_OK;
+    }
     kind = GramKind::BF16;
     gg = gb;
     goto again;
@@ -553,6 +566,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   // Algorithm and tile.
   PassCfg cfg{};
   int algo = o->algo;
+  bool panel_gram_rejected = false;
   const bool panels = o->layout == GM_LAYOUT_PANELS;
   if (o->layout != GM_LAYOUT_ROWS && !panels)
     return fail(GM_ERR_INVALID, "gm_weiszfeld_f32: unknown layout %d", o->layout);
@@ -566,9 +580,24 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
     if (ldx < K * W || (reinterpret_cast<uintptr_t>(X) & 15) || K * W * 4 > 0x7fffffff)
       return fail(GM_ERR_INVALID, "panel layout: need panel stride >= K*W (%lld), 16-byte aligned "
                   "X, K*W*4 < 2^31 (ldx=%lld)", (long long)(K * W), (long long)ldx);
+    // gm2 at K <= 256: the scaled-f16 Gram reads panels too (AUTO on large d, as
+    // for rows, guarded; explicit algo="gram" guarded likewise); streaming otherwise
+    const bool gram_ok = o->mode == GM_MODE_IDEAL && gram_kt(K) > 0 && W % 64 == 0 &&
+                         (W & (W - 1)) == 0;
+    if ((algo == GM_ALGO_AUTO && gram_ok && d_total >= (int64_t)1 << 18) ||
+        (algo == GM_ALGO_GRAM && gram_ok)) {
+      static const bool unguarded = getenv("GMAGG_GRAM_UNGUARDED") != nullptr;
+      bool rejected = false;
+      const int rc0 = run_gram(c, X, K, d, W, guess0, out, o, res, cfg, s, true,
+                               algo == GM_ALGO_AUTO || !unguarded, &rejected, ldx);
+      if (rc0 || !rejected) return rc0;
+      panel_gram_rejected = true;
+      algo = GM_ALGO_STREAM;
+    }
     if (algo == GM_ALGO_AUTO) algo = GM_ALGO_STREAM;
     if (algo != GM_ALGO_STREAM)
-      return fail(GM_ERR_UNSUPPORTED, "panel layout: streaming algorithm only (algo %d)", algo);
+      return fail(GM_ERR_UNSUPPORTED, "panel layout: streaming or (gm2, K <= 256) Gram only "
+                  "(algo %d)", algo);
   }
   const int V = panels ? 4 : pick_vec(X, d, ldx);
   // AUTO: Gram-space (split bf16) for gm2 at K <= 256 on large d, kept if its
@@ -579,7 +608,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   // contiguous shards of a d_total % 4 == 0 update always do.
   const bool gram_local_ok = gram_kt(K) > 0 && V == 4 && ldx < ((int64_t)1 << 26) &&
                              pick_cfg(K, V, ldx, &cfg);
-  bool guard_rejected = false;   // a Gram result was computed and refused by the guard
+  bool guard_rejected = panel_gram_rejected;   // a Gram result was computed and refused
   const bool gram_auto = algo == GM_ALGO_AUTO && o->mode == GM_MODE_IDEAL && !panels &&
                          gram_kt(K) > 0 && d_total >= (int64_t)1 << 18 &&
                          (sharded ? d_total % 4 == 0 : gram_local_ok);

@@ -132,9 +132,10 @@ struct GramGrid {
 int gram_kt(int64_t K);
 GramGrid gram_grid(int64_t d, GramKind kind, int num_cu);
 size_t gram_slab_floats(int KT, const GramGrid& g);
+// pstride > 0: X in the panel layout [ceil(d/W)][K][W], W = 1 << wshift (H16 only).
 hipError_t launch_gram(const float* X, int64_t K, int64_t d, int64_t ldx, const float* p,
                        GramKind kind, const GramGrid& g, float* slab, double* G, KState* st,
-                       hipStream_t s);
+                       hipStream_t s, int64_t pstride = 0, int wshift = 0);
 hipError_t launch_gram_check(const double* G, int KP, KState* st, hipStream_t s);
 hipError_t launch_gram_verify(const double* G, int KP, int64_t K, float eps, const double* u,
                               const double* alpha, const double* Dx, double* bvec, KState* st,

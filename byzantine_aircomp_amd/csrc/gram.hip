@@ -405,6 +405,9 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
+#ifndef GMK_H16_PROBE
+#define GMK_H16_PROBE 0       // timing-probe builds only (3: no LDS stores, 4: no LDS reads)
+#endif
 constexpr int kH16BK = 64;            // columns per stage
 constexpr int kH16LS = kH16BK + 8;    // LDS row stride (halves): 144 B
 constexpr int kH16Flush = 128;        // stages per fp32 partial
@@ -412,23 +415,25 @@ constexpr int kH16Flush = 128;        // stages per fp32 partial
 template <int KT>
 using H16Lds = _Float16[2][2][GramShape<KT>::KP * kH16LS];   // [buffer][h|m][row][col]
 
-template <int KT, int NS>
+template <int KT, int NS, bool PANEL>
 struct H16Stream {
   static constexpr int RPT = GramShape<KT>::ROWS_PER_THREAD;
   const float* X;
   const float* p;
   int64_t K, ldx, c_begin, c_end;
+  int64_t pstride;   // > 0: X in the panel layout [ceil(d/W)][K][W], W = 1 << wshift
+  int wshift;
   int r0, cg;
   uint32_t voff;   // byte offset of this lane's row r0 within a row group (same for all groups)
   f32x4 st[NS][RPT];
   f32x4 pc[NS];
   float cm[NS];    // 1 for a stage's real columns, 0 past c_end
-  float sc[RPT];   // 2^e_k for real rows, 0 for padding rows (>= K)
+  float sb;        // the block's scale 2^e
 
   // Row group i (rows 16i + r0) is a raw buffer resource in SGPRs at row 16i plus
   // the lane's VGPR offset r0 * ldx * 4 (the same for every full group).  Lanes
-  // past K read row 16i (or row 0 for a group wholly past K) and are zeroed by sc;
-  // columns past c_end re-read the stage's first columns, zeroed by cm.
+  // past K read row 16i (or row 0 for a group wholly past K); columns past c_end
+  // re-read the stage's first columns, zeroed by cm.
   __device__ __forceinline__ uint32_t stage_cols(int s, float& cmv) const {
     const int64_t c0 = c_begin + (int64_t)s * kH16BK;
     const bool cval = c0 + cg * 4 < c_end;
@@ -439,9 +444,16 @@ struct H16Stream {
     const int64_t c0 = c_begin + (int64_t)s * kH16BK;
     const int64_t rem = K - 16 * i;                        // wave-uniform
     const int64_t rb = rem > 0 ? 16 * i : 0;
-    const uint32_t off = (rem >= 16 || r0 < rem) ? voff + lb : lb;
+    // r0 <= 15: every lane of a full group (rem >= 16) is real; branch-free select
+    const uint32_t off = lb + (voff & (0u - (uint32_t)((int64_t)r0 < rem)));
+    // panels: a 64-column stage never straddles a panel (W a multiple of 64), and
+    // its rows are W floats apart: 256 B row segments 4W B apart, one ~4W*K-byte
+    // region per stage instead of K segments ldx floats apart
+    const float* base = PANEL ? X + (c0 >> wshift) * pstride + rb * ((int64_t)1 << wshift) +
+                                    (c0 & (((int64_t)1 << wshift) - 1))
+                              : X + c0 + rb * ldx;
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(X + c0 + rb * ldx), 0, -1, 0x00020000);
+        const_cast<float*>(base), 0, -1, 0x00020000);
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2));
   }
   __device__ __forceinline__ f32x4 load_p(int s, float cmv) const {
@@ -460,17 +472,30 @@ struct H16Stream {
     const f32x4 x = (st[SET][i] - pc[SET]) * cm[SET];
     return fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
   }
+  // y = (x - p) * 2^e as ONE fma per element: f = 2^e (0 past c_end), q = -p f,
+  // both per stage and lane.  Rows past K (lanes of a partial last row group) hold
+  // a duplicate of a real row: finite values whose G rows / columns >= K no K-space
+  // kernel reads.
   template <int SET>
-  __device__ __forceinline__ void commit_row(int i, _Float16* Lh, _Float16* Lm) {
-    const int r = r0 + 16 * i;
-    const f32x4 x = (st[SET][i] - pc[SET]) * (sc[i] * cm[SET]);
+  __device__ __forceinline__ void commit_row(int i, _Float16* Lh, _Float16* Lm, float f,
+                                             const f32x4& q) {
+    f32x4 x;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) x[v] = fmaf(st[SET][i][v], f, q[v]);
     const f32x2 x01 = {x[0], x[1]}, x23 = {x[2], x[3]};
     const f16x2 h01 = __builtin_convertvector(x01, f16x2);
     const f16x2 h23 = __builtin_convertvector(x23, f16x2);
     const f16x2 m01 = __builtin_convertvector(x01 - __builtin_convertvector(h01, f32x2), f16x2);
     const f16x2 m23 = __builtin_convertvector(x23 - __builtin_convertvector(h23, f32x2), f16x2);
-    *reinterpret_cast<f16x4*>(Lh + r * kH16LS + cg * 4) = f16x4{h01[0], h01[1], h23[0], h23[1]};
-    *reinterpret_cast<f16x4*>(Lm + r * kH16LS + cg * 4) = f16x4{m01[0], m01[1], m23[0], m23[1]};
+#if GMK_H16_PROBE == 3   // timing probe: the conversion without its LDS stores (wrong G)
+    asm volatile("" ::"v"(h01), "v"(h23), "v"(m01), "v"(m23));
+    (void)Lh; (void)Lm;
+#else
+    // Lh / Lm point at this lane's slot of row r0: row r0 + 16 i is a constant
+    // offset (fits the ds_write immediate: no per-row address arithmetic)
+    *reinterpret_cast<f16x4*>(Lh + 16 * i * kH16LS) = f16x4{h01[0], h01[1], h23[0], h23[1]};
+    *reinterpret_cast<f16x4*>(Lm + 16 * i * kH16LS) = f16x4{m01[0], m01[1], m23[0], m23[1]};
+#endif
   }
   // commit stage data of set SET into (Lh, Lm), re-issuing each row's registers
   // for stage sn right after its commit (rolling)
@@ -479,9 +504,13 @@ struct H16Stream {
     float cmn;
     const uint32_t lbn = stage_cols(sn, cmn);
     const f32x4 pcn = load_p(sn, cmn);
+    const float f = sb * cm[SET];
+    const f32x4 q = -pc[SET] * f;
+    _Float16* lh = Lh + r0 * kH16LS + cg * 4;
+    _Float16* lm = Lm + r0 * kH16LS + cg * 4;
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
-      commit_row<SET>(i, Lh, Lm);
+      commit_row<SET>(i, lh, lm, f, q);
       asm volatile("" ::: "memory");       // the re-issue stays behind this row's commit
       st[SET][i] = load_row(sn, i, lbn);
     }
@@ -510,8 +539,12 @@ __device__ __forceinline__ void h16_step_b(const _Float16* Lh, const _Float16* L
                                            f32x16 (&acc)[GramShape<KT>::PER_WAVE]) {
   if constexpr (B >= W) {
     using O = H16Order<KT, W>;
+#if GMK_H16_PROBE == 4   // timing probe: MFMAs on register fragments, no LDS reads (wrong G)
+    const f16x8 hb = haw * (_Float16)B, mb = maw * (_Float16)B;
+#else
     const f16x8 hb = *reinterpret_cast<const f16x8*>(Lh + B * 32 * kH16LS + off);
     const f16x8 mb = *reinterpret_cast<const f16x8*>(Lm + B * 32 * kH16LS + off);
+#endif
     constexpr int tw = O::slot_w(B);
     acc[tw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(haw, hb, acc[tw], 0, 0, 0);
     acc[tw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(haw, mb, acc[tw], 0, 0, 0);
@@ -529,11 +562,16 @@ __device__ __forceinline__ void h16_step_b(const _Float16* Lh, const _Float16* L
 template <int KT, int W>
 __device__ __forceinline__ void h16_step(const _Float16* Lh, const _Float16* Lm, int off,
                                          f32x16 (&acc)[GramShape<KT>::PER_WAVE]) {
+#if GMK_H16_PROBE == 4
+  const f16x8 haw = __builtin_bit_cast(f16x8, (int __attribute__((ext_vector_type(4)))){off, off + 1, off + 2, off + 3});
+  const f16x8 maw = haw * (_Float16)0.5f, hao = haw * (_Float16)0.25f, mao = haw * (_Float16)0.125f;
+#else
   constexpr int AO = KT == 1 ? 0 : KT - 1 - W;
   const f16x8 haw = *reinterpret_cast<const f16x8*>(Lh + W * 32 * kH16LS + off);
   const f16x8 maw = *reinterpret_cast<const f16x8*>(Lm + W * 32 * kH16LS + off);
   const f16x8 hao = *reinterpret_cast<const f16x8*>(Lh + AO * 32 * kH16LS + off);
   const f16x8 mao = *reinterpret_cast<const f16x8*>(Lm + AO * 32 * kH16LS + off);
+#endif
   h16_step_b<KT, W, KT - 1>(Lh, Lm, off, haw, maw, hao, mao, acc);
 }
 
@@ -543,19 +581,23 @@ __device__ __forceinline__ void h16_step(const _Float16* Lh, const _Float16* Lm,
 // need (the compiler spilled 50-300 VGPRs at every unroll >= 3 tried).
 constexpr int kH16Sets = 2;
 
-template <int KT, int DBG>
+template <int KT, int DBG, bool PANEL>
 __device__ __forceinline__ void h16_producer(const float* __restrict__ X, int64_t K, int64_t ldx,
+                                             int64_t pstride, int wshift,
                                              const float* __restrict__ p, int64_t c_begin,
                                              int64_t c_end, int nstage, H16Lds<KT>& lds,
-                                             int* s_exp) {
+                                             int* s_exp, float* s_bmax) {
   constexpr int RPT = GramShape<KT>::ROWS_PER_THREAD;
-  H16Stream<KT, kH16Sets> P;
+  H16Stream<KT, kH16Sets, PANEL> P;
   const int t = threadIdx.x - 256;
   P.X = X; P.p = p; P.K = K; P.ldx = ldx; P.c_begin = c_begin; P.c_end = c_end;
+  P.pstride = pstride; P.wshift = wshift;
   P.r0 = t >> 4; P.cg = t & 15;
-  P.voff = (uint32_t)P.r0 * (uint32_t)ldx * 4u;
+  P.voff = (uint32_t)P.r0 * (uint32_t)(pstride ? (1 << wshift) : ldx) * 4u;
   if (nstage == 0 || DBG == 2) {                 // no columns: meet the consumers' barriers
-    for (int s = 0; s <= (DBG == 2 ? nstage : 0); ++s) __syncthreads();   // DBG 2: no loads
+    if (DBG == 2)
+      for (int k = t; k < GramShape<KT>::KP; k += 256) s_exp[k] = 0;
+    for (int s = 0; s <= (DBG == 2 ? nstage : 0) + 1; ++s) __syncthreads();   // DBG 2: no loads
     return;
   }
   // Every fetch and commit is unconditional: a stage index past the end is
@@ -565,22 +607,25 @@ __device__ __forceinline__ void h16_producer(const float* __restrict__ X, int64_
   const int last = nstage - 1;
   P.template fetch<0>(0);
   P.template fetch<1>(min(1, last));
-  // per-row scale from the first two stages: the 16 lanes of a row group hold its
-  // 64 columns (lanes 16j .. 16j+15 share r0)
+  // the block's scale from the first two stages: max |x'| over its real rows and
+  // columns -> wave max -> the 4 producer waves through LDS (one extra barrier,
+  // matched by the consumers)
+  float mx = 0.f;
 #pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    float mx = fmaxf(P.template absmax<0>(i), P.template absmax<1>(i));
-    mx = fmaxf(mx, __shfl_xor(mx, 1, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 2, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 4, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 8, 16));
+  for (int i = 0; i < RPT; ++i)
+    if (P.r0 + 16 * i < K) mx = fmaxf(mx, fmaxf(P.template absmax<0>(i), P.template absmax<1>(i)));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if ((t & 63) == 0) s_bmax[t >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(s_bmax[0], s_bmax[1]), fmaxf(s_bmax[2], s_bmax[3]));
+  {
     int ex = 0;
     (void)frexpf(mx, &ex);                       // mx = f 2^ex, f in [0.5, 1)
     int e = (mx > 0.f && mx <= 3.0e38f) ? 4 - ex : 0;
     e = e < -100 ? -100 : (e > 100 ? 100 : e);
-    const bool real = P.r0 + 16 * i < K;
-    P.sc[i] = real ? ldexpf(1.f, e) : 0.f;
-    if (P.cg == 0) s_exp[P.r0 + 16 * i] = real ? e : 0;
+    P.sb = ldexpf(1.f, e);
+    for (int k = t; k < GramShape<KT>::KP; k += 256) s_exp[k] = e;
   }
   P.template commit_refetch<0>(lds[0][0], lds[0][1], min(2, last));
   __syncthreads();                               // stage 0 in buffer 0, exponents published
@@ -633,6 +678,7 @@ __device__ __forceinline__ void h16_consumer(int nstage, int nseg, float* __rest
     }
   };
   const int fo = (lane & 31) * kH16LS + (lane >> 5) * 8;   // fragment offset in a tile
+  __syncthreads();                                           // the producers' scale exchange
   __syncthreads();                                           // stage 0 is in buffer 0
   int seg = 0;
   for (int s = 0; s < nstage; ++s) {
@@ -649,20 +695,23 @@ __device__ __forceinline__ void h16_consumer(int nstage, int nseg, float* __rest
     for (; seg < nseg; ++seg) flush(seg, true);              // blocks with fewer stages
 }
 
-template <int KT, int DBG = 0>
+template <int KT, int DBG, bool PANEL>
 __global__ void __launch_bounds__(512, 1) gram_h16_partial(const float* __restrict__ X, int64_t K,
-                                                           int64_t d, int64_t ldx,
+                                                           int64_t d, int64_t ldx, int64_t pstride,
+                                                           int wshift,
                                                            const float* __restrict__ p,
                                                            int64_t cols_per_block, int nseg,
                                                            float* __restrict__ slab) {
   __shared__ H16Lds<KT> lds;
   __shared__ int s_exp[GramShape<KT>::KP];
+  __shared__ float s_bmax[4];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t c_begin = (int64_t)blockIdx.x * cols_per_block;
   const int64_t c_end = c_begin + cols_per_block < d ? c_begin + cols_per_block : d;
   const int nstage = c_begin < c_end ? (int)((c_end - c_begin + kH16BK - 1) / kH16BK) : 0;
   if (w >= 4) {
-    h16_producer<KT, DBG>(X, K, ldx, p, c_begin, c_end, nstage, lds, s_exp);
+    h16_producer<KT, DBG, PANEL>(X, K, ldx, pstride, wshift, p, c_begin, c_end, nstage, lds, s_exp,
+                          s_bmax);
     return;
   }
   if constexpr (KT == 8) {
@@ -890,20 +939,30 @@ static hipError_t launch_split_kt(const float* X, int64_t K, int64_t d, int64_t 
   return hipGetLastError();
 }
 
+template <int KT, int DBG>
+static void launch_h16_dbg(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t pstride,
+                           int wshift, const float* p, int nb, int64_t cpb, int nseg, float* slab,
+                           hipStream_t s) {
+  if (pstride)
+    hipLaunchKernelGGL((gram_h16_partial<KT, DBG, true>), dim3(nb), dim3(512), 0, s, X, K, d, ldx,
+                       pstride, wshift, p, cpb, nseg, slab);
+  else
+    hipLaunchKernelGGL((gram_h16_partial<KT, DBG, false>), dim3(nb), dim3(512), 0, s, X, K, d, ldx,
+                       pstride, wshift, p, cpb, nseg, slab);
+}
+
 template <int KT>
-static hipError_t launch_h16_kt(const float* X, int64_t K, int64_t d, int64_t ldx, const float* p,
-                                int nb, int64_t cpb, int nseg, float* slab, hipStream_t s) {
+static hipError_t launch_h16_kt(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t pstride,
+                                int wshift, const float* p, int nb, int64_t cpb, int nseg,
+                                float* slab, hipStream_t s) {
   // GMAGG_GRAM_DEBUG = 1 / 2: timing probes without MFMAs / without loads (wrong G)
   static const int dbg = [] { const char* e = getenv("GMAGG_GRAM_DEBUG"); return e ? atoi(e) : 0; }();
   if (dbg == 1)
-    hipLaunchKernelGGL((gram_h16_partial<KT, 1>), dim3(nb), dim3(512), 0, s, X, K, d, ldx, p, cpb,
-                       nseg, slab);
+    launch_h16_dbg<KT, 1>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, s);
   else if (dbg == 2)
-    hipLaunchKernelGGL((gram_h16_partial<KT, 2>), dim3(nb), dim3(512), 0, s, X, K, d, ldx, p, cpb,
-                       nseg, slab);
+    launch_h16_dbg<KT, 2>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, s);
   else
-    hipLaunchKernelGGL((gram_h16_partial<KT, 0>), dim3(nb), dim3(512), 0, s, X, K, d, ldx, p, cpb,
-                       nseg, slab);
+    launch_h16_dbg<KT, 0>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, s);
   return hipGetLastError();
 }
 
@@ -934,17 +993,18 @@ GramGrid gram_grid(int64_t d, GramKind kind, int num_cu) {
 
 hipError_t launch_gram(const float* X, int64_t K, int64_t d, int64_t ldx, const float* p,
                        GramKind kind, const GramGrid& g, float* slab, double* G, KState* st,
-                       hipStream_t s) {
+                       hipStream_t s, int64_t pstride, int wshift) {
+  if (pstride && kind != GramKind::H16) return hipErrorInvalidValue;   // panels: f16 kernel only
   const int KT = gram_kt(K);
   const int nb = g.nb;
   const int64_t cpb = g.cpb;
   hipError_t e;
   if (kind == GramKind::H16) {
     switch (KT) {
-      case 1: e = launch_h16_kt<1>(X, K, d, ldx, p, nb, cpb, g.nseg, slab, s); break;
-      case 2: e = launch_h16_kt<2>(X, K, d, ldx, p, nb, cpb, g.nseg, slab, s); break;
-      case 4: e = launch_h16_kt<4>(X, K, d, ldx, p, nb, cpb, g.nseg, slab, s); break;
-      case 8: e = launch_h16_kt<8>(X, K, d, ldx, p, nb, cpb, g.nseg, slab, s); break;
+      case 1: e = launch_h16_kt<1>(X, K, d, ldx, pstride, wshift, p, nb, cpb, g.nseg, slab, s); break;
+      case 2: e = launch_h16_kt<2>(X, K, d, ldx, pstride, wshift, p, nb, cpb, g.nseg, slab, s); break;
+      case 4: e = launch_h16_kt<4>(X, K, d, ldx, pstride, wshift, p, nb, cpb, g.nseg, slab, s); break;
+      case 8: e = launch_h16_kt<8>(X, K, d, ldx, pstride, wshift, p, nb, cpb, g.nseg, slab, s); break;
       default: return hipErrorInvalidValue;
     }
   } else {

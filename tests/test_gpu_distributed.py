@@ -79,7 +79,8 @@ def test_sharded_gm2_world1(world1, transport, layout):
 
 
 @pytest.mark.parametrize("transport", ["rccl", "torch"])
-def test_sharded_gram_world1(world1, transport):
+@pytest.mark.parametrize("layout", ["rows", "panels"])
+def test_sharded_gram_world1(world1, transport, layout):
     """AUTO at K <= 256 on a d_total >= 2^18 update: the Gram path's two all-reduces
     (G, then the guard's sums) through the process group."""
     import byzantine_aircomp_amd as bz
@@ -91,7 +92,8 @@ def test_sharded_gram_world1(world1, transport):
     n = bz.aggregators.last_result.iters
     sg = ShardedGM(d, transport=transport)
     try:
-        got = sg.gm2(X, dict(opts))
+        Xin = bz.ClientPanels.from_rows(X) if layout == "panels" else X
+        got = sg.gm2(Xin, dict(opts))
         torch.cuda.synchronize()
         res = sg.last_result
     finally:

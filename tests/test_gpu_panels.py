@@ -11,6 +11,7 @@ import pytest
 import torch
 
 from conftest import golden_case, golden_names, rel_l2
+from oracle import aggregators as orc
 
 pytestmark = pytest.mark.gpu
 
@@ -92,11 +93,21 @@ def test_panels_store_rows_and_default_guess():
 
 
 def test_panels_reject_non_streaming_algos():
+    """Panels run the streaming pass or (gm2, K <= 256) the f16 Gram; the other
+    algorithms, the f32 Gram, and Gram for AirComp gm or K > 256 raise."""
     X, g0 = _data(64, 512, seed=1)
     P = bz().ClientPanels.from_rows(X)
-    for algo in ("gram", "twopass", "resident"):
+    for algo in ("twopass", "resident", "gram_f32"):
         with pytest.raises(RuntimeError):
             bz().gm2(P, {"maxiter": 5, "guess": g0, "algo": algo})
+    with pytest.raises(RuntimeError):
+        bz().gm(P, {"maxiter": 5, "guess": g0, "algo": "gram", "noise_var": 1e-2})
+    X2, g2 = _data(300, 512, seed=2)
+    with pytest.raises(RuntimeError):
+        bz().gm2(bz().ClientPanels.from_rows(X2), {"maxiter": 5, "guess": g2, "algo": "gram"})
+    # gm2 at K <= 256: explicit Gram on panels is supported (guarded)
+    out = bz().gm2(P, {"maxiter": 5, "guess": g0, "algo": "gram"})
+    assert bz().aggregators.last_result.algo in ("gram", "stream") and out.shape == (512,)
 
 
 @pytest.mark.parametrize("K,d", [(50, 7850), (1000, 4099), (300, 257)])
@@ -132,3 +143,49 @@ def test_rows_to_panels_kernel_matches_layout(K, d, W, offset):
     ref = ref.view(K, npan, Wd).transpose(0, 1)
     assert torch.equal(P.data.cpu(), ref)
     assert torch.equal(P.to_rows().cpu(), X.cpu())
+
+
+@pytest.mark.parametrize("K,d", [(256, 1 << 18), (200, (1 << 18) + 4160), (64, (1 << 18) + 36),
+                                 (33, 300_000), (1, 1 << 18)])
+def test_gram_on_panels_matches_rows_and_stream(K, d):
+    """gm2 at K <= 256 on ClientPanels: AUTO takes the scaled-f16 Gram straight from
+    the panel layout (W-column panels, 64-column stages), guarded; it agrees with
+    the row-major Gram and with the streaming path."""
+    m = bz()
+    g = torch.Generator().manual_seed(K + d)
+    X = 0.05 * torch.randn(K, d, generator=g)
+    B = K // 5
+    if B:
+        X[K - B:] = 0.25 + 0.5 * torch.randn(B, d, generator=g)
+    X, g0 = X.cuda(), (0.01 * torch.randn(d, generator=g)).cuda()
+    P = m.ClientPanels.from_rows(X)
+    opts = {"maxiter": 1000, "tol": 1e-5, "guess": g0}
+    a = m.gm2(P, dict(opts))
+    ra = m.aggregators.last_result
+    assert ra.algo == "gram" and ra.guard == "accepted" and ra.gram_kind == "f16_split"
+    b = m.gm2(X, dict(opts, algo="gram"))
+    rb = m.aggregators.last_result
+    assert rb.algo == "gram" and ra.iters == rb.iters
+    assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 1e-6
+    c = m.gm2(P, dict(opts, algo="stream"))
+    assert abs(m.aggregators.last_result.iters - ra.iters) <= 1
+    assert rel_l2(a.cpu().numpy(), c.cpu().numpy()) <= 1e-5
+
+
+def test_gram_on_panels_overflow_falls_back_to_stream():
+    """An element past the f16 headroom on panels: no bf16 panel kernel, so the
+    call ends on the streaming path (guard 'rejected') and still matches."""
+    m = bz()
+    g = torch.Generator().manual_seed(5)
+    K, d = 64, 1 << 18
+    X = 0.05 * torch.randn(K, d, generator=g)
+    X[K - 12:] += 0.25
+    X[5, 200_000] = 1e6
+    p = torch.zeros(d)
+    want, tr = orc.gm2(X.clone(), {"maxiter": 1000, "tol": 1e-5, "guess": p})
+    P = m.ClientPanels.from_rows(X.cuda())
+    got = m.gm2(P, {"maxiter": 1000, "tol": 1e-5, "guess": p.cuda()})
+    res = m.aggregators.last_result
+    assert res.algo == "stream" and res.guard == "rejected"
+    assert rel_l2(got.cpu().numpy(), want.numpy()) <= 1e-5
+    assert abs(res.iters - tr.iters) <= 1
