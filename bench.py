@@ -136,6 +136,10 @@ def pmc_traffic(workload, layout, kernel="weiszfeld_pass", mode="0"):
                 panel = len(targs) == 8 and targs[7] == "true"
                 if targs[4] == mode and panel == (layout == "panels"):
                     return row["hbm_bytes_per_launch"] / 1e9, os.path.relpath(path, ROOT)
+            elif kernel == "gram_h16_partial":
+                m = re.search(r"gram_h16_partial<([^>]*)>", name)
+                if m and m.group(1).split(", ")[-1] == ("true" if layout == "panels" else "false"):
+                    return row["hbm_bytes_per_launch"] / 1e9, os.path.relpath(path, ROOT)
             elif kernel in name:
                 return row["hbm_bytes_per_launch"] / 1e9, os.path.relpath(path, ROOT)
     return None, None
@@ -514,25 +518,32 @@ def main():
         agg_frac = passes * per_launch_bytes / agg_s / 1e9 / HBM_PEAK_GBS
         if res.algo in ("gram", "gram_f32"):
             # dominant kernel = the Gram partial: upper-triangle 32x32 tiles of the
-            # K-padded Gram, 2 FLOP per MAC, d_local columns; the split kernel issues
-            # 4 bf16 MFMAs (hh, hm, mh, mm) per tile and 16 columns.  It also reads X
-            # once: price both ceilings and report the binding one.
+            # K-padded Gram, 2 FLOP per MAC, d_local columns.  The scaled-f16 split
+            # (gram_kind f16_split) issues 3 f16 MFMAs per tile and 16 columns (hh, hm, mh),
+            # the bf16 fallback 4 (hh, hm, mh, mm), gram_f32 one f32 MFMA.  It also reads
+            # X once: price both ceilings and report the binding one.
             kt = 1 if K <= 32 else 2 if K <= 64 else 4 if K <= 128 else 8
             split = res.algo == "gram"
-            flops = kt * (kt + 1) / 2 * 1024 * 2.0 * d * (4 if split else 1)
+            h16 = split and res.gram_kind == "f16_split"
+            products = 3 if h16 else 4 if split else 1
+            flops = kt * (kt + 1) / 2 * 1024 * 2.0 * d * products
             peak = MFMA_BF16_PEAK_TFLOPS if split else MFMA_F32_PEAK_TFLOPS
             tf = flops / avg_pass_s / 1e12
             gbs = per_launch_bytes / avg_pass_s / 1e9
-            traffic, traffic_src = pmc_traffic(args.workload, layout, "gram_split_partial") \
+            kname = "gram_h16_partial" if h16 else "gram_split_partial"
+            traffic, traffic_src = pmc_traffic(args.workload, layout, kname) \
                 if world == 1 and split else (None, None)
             mf = {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s",
                   "frac": tf / peak, "traffic": traffic}
             hb = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": gbs / HBM_PEAK_GBS, "traffic": traffic}
             roof, other = (mf, hb) if mf["frac"] >= hb["frac"] else (hb, mf)
-            roof.update({"kernel": ("gram_split_partial (v_mfma_f32_32x32x16_bf16, h+m split, "
+            roof.update({"kernel": (f"gram_h16_partial ({layout}; v_mfma_f32_32x32x16_f16 x3, "
+                                    "scaled h+m split, upper-triangle tiles)") if h16 else
+                                   ("gram_split_partial (v_mfma_f32_32x32x16_bf16 x4, h+m split, "
                                     "upper-triangle tiles)") if split else
                                    "gram_partial (v_mfma_f32_32x32x2_f32, upper-triangle tiles)",
+                         "gram_kind": res.gram_kind,
                          "traffic_unit": "GB per launch", "traffic_source": traffic_src,
                          "launches_timed": launches, "avg_launch_us": avg_pass_s * 1e6,
                          "algorithmic_flops_per_launch": flops,

@@ -29,8 +29,7 @@ namespace gmk {
 template <int V, int R>
 struct Tile {
   float x[R][V];
-  float g[V];    // INIT: the guess at this lane's columns
-  float gold;    // STEP finisher thread: g_t at its column
+  float gold;    // finisher thread: g_t at its column (INIT: the guess)
   float hn;      // STEP finisher thread, host noise: its column's draw
 };
 
@@ -57,7 +56,7 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
   using T = Tile<V, R>;
 
   __shared__ float s_red[NW][J];
-  __shared__ float s_g[J];
+  __shared__ float s_g[INIT ? 2 : 1][J];   // INIT: by chunk parity (one barrier per chunk)
   __shared__ double s_fin[2][NW];
   __shared__ float s_w[OCC > 1 ? NW * QW * R : 1];
 
@@ -72,8 +71,6 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
     a.seed += (uint64_t)pb * kSeedStride;
   }
   if (!SUM_ONLY && a.st->done) return;
-  // INIT reads the guess per lane: as one dwordx4 when it is 16-byte aligned
-  const bool g_vec = V > 1 && (reinterpret_cast<uintptr_t>(a.g_old) & (4 * V - 1)) == 0;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -137,30 +134,14 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
       for (int v = 0; v < V; ++v) t.x[i][v] = 0.f;
     }
   };
+  // The column-wise operands ride with the chunk on the J finisher threads (one
+  // register each), not on every lane: INIT then costs the registers STEP does,
+  // and both take the rolling prefetch without spilling.
   auto fetch_aux = [&](int64_t ch, T& t) {
-    if constexpr (INIT) {
-      const int64_t col = ch * J + (int64_t)c * V;
-      const bool cval = ch < nch && col < d;
-      if (V > 1 && (ch + 1) * J <= d && g_vec) {   // full chunk, aligned guess: one load per lane
-        if constexpr (V > 1) {
-          typedef typename vec<V>::t GV;
-          const GV gv4 = *reinterpret_cast<const GV*>(a.g_old + col);
-#pragma unroll
-          for (int v = 0; v < V; ++v) t.g[v] = gv4[v];
-        }
-      } else if (!PANEL || (ch + 1) * J <= d) {   // row-major: V | d, groups all-in or all-out
-#pragma unroll
-        for (int v = 0; v < V; ++v) t.g[v] = cval ? a.g_old[col + v] : 0.f;
-      } else {                             // panels: d need not be a multiple of V
-#pragma unroll
-        for (int v = 0; v < V; ++v) t.g[v] = (ch < nch && col + v < d) ? a.g_old[col + v] : 0.f;
-      }
-    } else {
-      const int64_t gj = ch * J + tid;
-      const bool fin = tid < J && ch < nch && gj < d;
-      t.gold = fin ? a.g_old[gj] : 0.f;
-      t.hn = (fin && a.noise == 2) ? a.hnoise[gj] : 0.f;
-    }
+    const int64_t gj = ch * J + tid;
+    const bool fin = tid < J && ch < nch && gj < d;
+    t.gold = fin ? a.g_old[gj] : 0.f;
+    if constexpr (!INIT) t.hn = (fin && a.noise == 2) ? a.hnoise[gj] : 0.f;
   };
   auto fetch = [&](int64_t ch, T& t) {
 #pragma unroll
@@ -176,15 +157,20 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
   // ROLL: row i of chunk `nxt` is loaded into t.x[i] as soon as phase B has
   // consumed row i of chunk ch, so the next chunk's loads are in flight during
   // phase B, the row reductions and the next chunk's barriers (no second tile).
+  int par = 0;   // INIT: chunk parity -> s_g buffer
   auto process = [&](int64_t ch, T& t, int64_t nxt) {
     float gv[V];
     if constexpr (INIT) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) gv[v] = t.g[v];
-      if (w == 0 && q == 0) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) gn_acc += (double)(gv[v] * gv[v]);
+      // the guess at this chunk's columns -> LDS (buffer by parity: a thread still
+      // reading the previous chunk's buffer has not passed this chunk's barrier)
+      if (tid < J) {
+        s_g[par][tid] = t.gold;
+        gn_acc += (double)(t.gold * t.gold);
       }
+      __syncthreads();
+#pragma unroll
+      for (int v = 0; v < V; ++v) gv[v] = s_g[par][c * V + v];
+      par ^= 1;
     } else {
       // phase A: weighted column sums over this thread's rows ...
       float acc[V];
@@ -227,11 +213,11 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
           mv_acc += (double)(diff * diff);
           gn_acc += (double)(gnew * gnew);
         }
-        s_g[tid] = gnew;
+        s_g[0][tid] = gnew;
       }
       __syncthreads();
 #pragma unroll
-      for (int v = 0; v < V; ++v) gv[v] = s_g[c * V + v];
+      for (int v = 0; v < V; ++v) gv[v] = s_g[0][c * V + v];
     }
     if constexpr (SUM_ONLY) {
       if constexpr (ROLL) fetch(nxt, t);
@@ -344,13 +330,15 @@ static const void* pass_fn(bool panel) {
   // Measured on MI355X (profiles/r01_ab_pass.txt, r01_pipe_sweep.txt): the plain
   // pass is as fast or faster than the two-tile PIPE variant at every K, so that
   // one is only built with -DGMK_PIPE_VARIANT for A/B runs.
-  // Panels: the rolling-prefetch STEP pass (6.44-6.56 vs 6.63 ms at C3); its INIT
-  // variants spill (29 VGPRs at the C3 tile) and run slower, so INIT stays plain
-  // (profiles/r03_panels_ab.txt).
+  // Panels: the rolling-prefetch STEP pass (6.44-6.56 vs 6.63 ms at C3).  INIT stays
+  // plain: with the guess on the finisher threads (one load per column instead of
+  // one per lane) plain INIT runs at STEP's time, 6.33 vs 6.33 ms, and the rolling
+  // INIT gains nothing, 6.29-6.65 vs STEP 6.32-6.56 (profiles/r2_init_ab.txt).
+  constexpr bool kRollDefault = MODE == 0;
   if constexpr (V == 4) {
     if (panel) {
       const int pv = pass_variant();
-      if (pv == 2 || (pv < 0 && MODE == 0))
+      if (pv == 2 || (pv < 0 && kRollDefault))
         return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 2, OCC, true>);
       return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 0, OCC, true>);
     }
@@ -363,7 +351,7 @@ static const void* pass_fn(bool panel) {
 #endif
   // Row-major STEP passes with float4 rows also take the rolling prefetch: C5's
   // batched K=50 tile streams 4.64 vs 4.43 TB/s (profiles/r04_c5_roll_ab.txt).
-  if (pass_variant() == 2 || (pass_variant() < 0 && MODE == 0 && V == 4))
+  if (pass_variant() == 2 || (pass_variant() < 0 && kRollDefault && V == 4))
     return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 2, OCC>);
   return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 0, OCC>);
 }
