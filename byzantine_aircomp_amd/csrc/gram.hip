@@ -408,6 +408,19 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 #ifndef GMK_H16_PROBE
 #define GMK_H16_PROBE 0       // timing-probe builds only (3: no LDS stores, 4: no LDS reads)
 #endif
+#ifndef GMK_H16_MIX
+#define GMK_H16_MIX 1         // 0: the residual by convert-back + subtract (A/B builds)
+#endif
+// m = f16(y - h) for the two halves of h = f16(y0, y1): one v_fma_mix per element
+// (y - h is exact in the mixed FMA, then ONE rounding to f16: the same bits as the
+// f32 subtract + convert, at a third of the instructions; checked bit for bit by
+// tools/mixcheck.hip).  The compiler selects no fma_mix for this pattern itself.
+__device__ __forceinline__ f16x2 f16_residual(f16x2 h, float y0, float y1) {
+  uint32_t m;
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(m) : "v"(h), "v"(y0));
+  asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(m) : "v"(h), "v"(y1));
+  return __builtin_bit_cast(f16x2, m);
+}
 constexpr int kH16BK = 64;            // columns per stage
 constexpr int kH16LS = kH16BK + 8;    // LDS row stride (halves): 144 B
 constexpr int kH16Flush = 128;        // stages per fp32 partial
@@ -430,31 +443,41 @@ struct H16Stream {
   float cm[NS];    // 1 for a stage's real columns, 0 past c_end
   float sb;        // the block's scale 2^e
 
-  // Row group i (rows 16i + r0) is a raw buffer resource in SGPRs at row 16i plus
-  // the lane's VGPR offset r0 * ldx * 4 (the same for every full group).  Lanes
-  // past K read row 16i (or row 0 for a group wholly past K); columns past c_end
-  // re-read the stage's first columns, zeroed by cm.
+  // Row-major: row group i (rows 16i + r0) is a raw buffer resource in SGPRs at row
+  // 16i plus the lane's VGPR offset r0 * ldx * 4 (the same for every full group);
+  // lanes past K read row 16i (or row 0 for a group wholly past K).  Panels: ONE
+  // resource per stage, sized to the panel's K rows, and the row in the lane offset
+  // (rows past K read 0 from the range check; 16 SGPR resources per stage spilled).
+  // Columns past c_end re-read the stage's first columns, zeroed by cm.
   __device__ __forceinline__ uint32_t stage_cols(int s, float& cmv) const {
     const int64_t c0 = c_begin + (int64_t)s * kH16BK;
     const bool cval = c0 + cg * 4 < c_end;
     cmv = cval ? 1.f : 0.f;
     return cval ? (uint32_t)(cg * 16) : 0u;
   }
-  __device__ __forceinline__ f32x4 load_row(int s, int i, uint32_t lb) const {
+  // lb: stage_cols' column offset; returns the lane offset load_row takes
+  __device__ __forceinline__ uint32_t stage_off(uint32_t lb) const {
+    return PANEL ? lb + voff : lb;
+  }
+  __device__ __forceinline__ f32x4 load_row(int s, int i, uint32_t lo) const {
     const int64_t c0 = c_begin + (int64_t)s * kH16BK;
-    const int64_t rem = K - 16 * i;                        // wave-uniform
-    const int64_t rb = rem > 0 ? 16 * i : 0;
-    // r0 <= 15: every lane of a full group (rem >= 16) is real; branch-free select
-    const uint32_t off = lb + (voff & (0u - (uint32_t)((int64_t)r0 < rem)));
-    // panels: a 64-column stage never straddles a panel (W a multiple of 64), and
-    // its rows are W floats apart: 256 B row segments 4W B apart, one ~4W*K-byte
-    // region per stage instead of K segments ldx floats apart
-    const float* base = PANEL ? X + (c0 >> wshift) * pstride + rb * ((int64_t)1 << wshift) +
-                                    (c0 & (((int64_t)1 << wshift) - 1))
-                              : X + c0 + rb * ldx;
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(base), 0, -1, 0x00020000);
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2));
+    if constexpr (PANEL) {
+      // a 64-column stage never straddles a panel (W a multiple of 64); its rows
+      // are W floats apart: 256 B row segments 4W B apart, K * 4W bytes per stage
+      const float* base = X + (c0 >> wshift) * pstride + (c0 & (((int64_t)1 << wshift) - 1));
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(base), 0, (int)(K << (wshift + 2)), 0x00020000);
+      return __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lo + ((uint32_t)i << (wshift + 6)), 0, 2));
+    } else {
+      const int64_t rem = K - 16 * i;                      // wave-uniform
+      const int64_t rb = rem > 0 ? 16 * i : 0;
+      // r0 <= 15: every lane of a full group (rem >= 16) is real; branch-free select
+      const uint32_t off = lo + (voff & (0u - (uint32_t)((int64_t)r0 < rem)));
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(X + c0 + rb * ldx), 0, -1, 0x00020000);
+      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2));
+    }
   }
   __device__ __forceinline__ f32x4 load_p(int s, float cmv) const {
     const int64_t c0 = c_begin + (int64_t)s * kH16BK;
@@ -462,10 +485,10 @@ struct H16Stream {
   }
   template <int SET>
   __device__ __forceinline__ void fetch(int s) {
-    const uint32_t lb = stage_cols(s, cm[SET]);
+    const uint32_t lo = stage_off(stage_cols(s, cm[SET]));
     pc[SET] = load_p(s, cm[SET]);
 #pragma unroll
-    for (int i = 0; i < RPT; ++i) st[SET][i] = load_row(s, i, lb);
+    for (int i = 0; i < RPT; ++i) st[SET][i] = load_row(s, i, lo);
   }
   template <int SET>
   __device__ __forceinline__ float absmax(int i) const {
@@ -485,8 +508,13 @@ struct H16Stream {
     const f32x2 x01 = {x[0], x[1]}, x23 = {x[2], x[3]};
     const f16x2 h01 = __builtin_convertvector(x01, f16x2);
     const f16x2 h23 = __builtin_convertvector(x23, f16x2);
+#if GMK_H16_MIX
+    const f16x2 m01 = f16_residual(h01, x[0], x[1]);
+    const f16x2 m23 = f16_residual(h23, x[2], x[3]);
+#else
     const f16x2 m01 = __builtin_convertvector(x01 - __builtin_convertvector(h01, f32x2), f16x2);
     const f16x2 m23 = __builtin_convertvector(x23 - __builtin_convertvector(h23, f32x2), f16x2);
+#endif
 #if GMK_H16_PROBE == 3   // timing probe: the conversion without its LDS stores (wrong G)
     asm volatile("" ::"v"(h01), "v"(h23), "v"(m01), "v"(m23));
     (void)Lh; (void)Lm;
@@ -502,7 +530,7 @@ struct H16Stream {
   template <int SET>
   __device__ __forceinline__ void commit_refetch(_Float16* Lh, _Float16* Lm, int sn) {
     float cmn;
-    const uint32_t lbn = stage_cols(sn, cmn);
+    const uint32_t lon = stage_off(stage_cols(sn, cmn));
     const f32x4 pcn = load_p(sn, cmn);
     const float f = sb * cm[SET];
     const f32x4 q = -pc[SET] * f;
@@ -512,7 +540,7 @@ struct H16Stream {
     for (int i = 0; i < RPT; ++i) {
       commit_row<SET>(i, lh, lm, f, q);
       asm volatile("" ::: "memory");       // the re-issue stays behind this row's commit
-      st[SET][i] = load_row(sn, i, lbn);
+      st[SET][i] = load_row(sn, i, lon);
     }
     pc[SET] = pcn;
     cm[SET] = cmn;
