@@ -408,6 +408,9 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 #ifndef GMK_H16_PROBE
 #define GMK_H16_PROBE 0       // timing-probe builds only (3: no LDS stores, 4: no LDS reads)
 #endif
+#ifndef GMK_H16_DIAG
+#define GMK_H16_DIAG 1        // diagonal tiles in 2 MFMA products (0: 3, A/B builds)
+#endif
 #ifndef GMK_H16_MIX
 #define GMK_H16_MIX 1         // 0: the residual by convert-back + subtract (A/B builds)
 #endif
@@ -428,16 +431,28 @@ constexpr int kH16Flush = 128;        // stages per fp32 partial
 template <int KT>
 using H16Lds = _Float16[2][2][GramShape<KT>::KP * kH16LS];   // [buffer][h|m][row][col]
 
-template <int KT, int NS, bool PANEL>
+// WS = 0: X row-major; WS > 0: the panel layout [ceil(d/W)][K][W], W = 1 << WS.
+template <int KT, int NS, int WS>
 struct H16Stream {
+  static constexpr bool PANEL = WS > 0;
   static constexpr int RPT = GramShape<KT>::ROWS_PER_THREAD;
+  // Rows of a producer thread (r0 = 0..15).  Row-major: rows 16 i + r0 (one resource
+  // per row group).  Panels: runs of RUN consecutive rows, r0 * RUN + j in run q at
+  // q * RSTRIDE, so a row's byte offset in the stage is a constant that mostly fits
+  // the load's immediate field, and the 16-lane halves of a ds_write hit disjoint
+  // banks (rows 8 apart: 288 dwords, 32 banks off).
+  static constexpr int RUN = RPT < 8 ? RPT : 8;
+  static constexpr int RSTRIDE = GramShape<KT>::KP / (RPT / RUN);
+  static __device__ __forceinline__ constexpr int prow(int i) {   // panels: row - r0 * RUN
+    return (i / RUN) * RSTRIDE + i % RUN;
+  }
   const float* X;
   const float* p;
   int64_t K, ldx, c_begin, c_end;
-  int64_t pstride;   // > 0: X in the panel layout [ceil(d/W)][K][W], W = 1 << wshift
-  int wshift;
+  int64_t pstride;   // panels: elements between panels (>= K * W)
   int r0, cg;
-  uint32_t voff;   // byte offset of this lane's row r0 within a row group (same for all groups)
+  uint32_t voff;   // byte offset of this lane's first row (row-major: within a row group)
+  __device__ __forceinline__ int row(int i) const { return PANEL ? r0 * RUN + prow(i) : 16 * i + r0; }
   f32x4 st[NS][RPT];
   f32x4 pc[NS];
   float cm[NS];    // 1 for a stage's real columns, 0 past c_end
@@ -447,8 +462,8 @@ struct H16Stream {
   // 16i plus the lane's VGPR offset r0 * ldx * 4 (the same for every full group);
   // lanes past K read row 16i (or row 0 for a group wholly past K).  Panels: ONE
   // resource per stage, sized to the panel's K rows, and the row in the lane offset
-  // (rows past K read 0 from the range check; 16 SGPR resources per stage spilled).
-  // Columns past c_end re-read the stage's first columns, zeroed by cm.
+  // + a constant (rows past K read 0 from the range check; 16 SGPR resources per
+  // stage spilled).  Columns past c_end re-read the stage's first columns, zeroed by cm.
   __device__ __forceinline__ uint32_t stage_cols(int s, float& cmv) const {
     const int64_t c0 = c_begin + (int64_t)s * kH16BK;
     const bool cval = c0 + cg * 4 < c_end;
@@ -464,11 +479,11 @@ struct H16Stream {
     if constexpr (PANEL) {
       // a 64-column stage never straddles a panel (W a multiple of 64); its rows
       // are W floats apart: 256 B row segments 4W B apart, K * 4W bytes per stage
-      const float* base = X + (c0 >> wshift) * pstride + (c0 & (((int64_t)1 << wshift) - 1));
+      const float* base = X + (c0 >> WS) * pstride + (c0 & ((1 << WS) - 1));
       const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<float*>(base), 0, (int)(K << (wshift + 2)), 0x00020000);
+          const_cast<float*>(base), 0, (int)(K << (WS + 2)), 0x00020000);
       return __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lo + ((uint32_t)i << (wshift + 6)), 0, 2));
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lo + ((uint32_t)prow(i) << (WS + 2)), 0, 2));
     } else {
       const int64_t rem = K - 16 * i;                      // wave-uniform
       const int64_t rb = rem > 0 ? 16 * i : 0;
@@ -519,10 +534,11 @@ struct H16Stream {
     asm volatile("" ::"v"(h01), "v"(h23), "v"(m01), "v"(m23));
     (void)Lh; (void)Lm;
 #else
-    // Lh / Lm point at this lane's slot of row r0: row r0 + 16 i is a constant
-    // offset (fits the ds_write immediate: no per-row address arithmetic)
-    *reinterpret_cast<f16x4*>(Lh + 16 * i * kH16LS) = f16x4{h01[0], h01[1], h23[0], h23[1]};
-    *reinterpret_cast<f16x4*>(Lm + 16 * i * kH16LS) = f16x4{m01[0], m01[1], m23[0], m23[1]};
+    // Lh / Lm point at this lane's slot of its first row: row i is a constant offset
+    // (fits the ds_write immediate: no per-row address arithmetic)
+    const int rr = PANEL ? prow(i) : 16 * i;
+    *reinterpret_cast<f16x4*>(Lh + rr * kH16LS) = f16x4{h01[0], h01[1], h23[0], h23[1]};
+    *reinterpret_cast<f16x4*>(Lm + rr * kH16LS) = f16x4{m01[0], m01[1], m23[0], m23[1]};
 #endif
   }
   // commit stage data of set SET into (Lh, Lm), re-issuing each row's registers
@@ -534,8 +550,8 @@ struct H16Stream {
     const f32x4 pcn = load_p(sn, cmn);
     const float f = sb * cm[SET];
     const f32x4 q = -pc[SET] * f;
-    _Float16* lh = Lh + r0 * kH16LS + cg * 4;
-    _Float16* lm = Lm + r0 * kH16LS + cg * 4;
+    _Float16* lh = Lh + (PANEL ? r0 * RUN : r0) * kH16LS + cg * 4;
+    _Float16* lm = Lm + (PANEL ? r0 * RUN : r0) * kH16LS + cg * 4;
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
       commit_row<SET>(i, lh, lm, f, q);
@@ -574,14 +590,26 @@ __device__ __forceinline__ void h16_step_b(const _Float16* Lh, const _Float16* L
     const f16x8 mb = *reinterpret_cast<const f16x8*>(Lm + B * 32 * kH16LS + off);
 #endif
     constexpr int tw = O::slot_w(B);
-    acc[tw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(haw, hb, acc[tw], 0, 0, 0);
-    acc[tw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(haw, mb, acc[tw], 0, 0, 0);
-    acc[tw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(maw, hb, acc[tw], 0, 0, 0);
+    if constexpr (GMK_H16_DIAG && B == W) {
+      // diagonal tile: h h^T + h (2m)^T = hh^T + 2 S, S = h m^T; its symmetric part
+      // is hh^T + S + S^T, taken by gram_reduce_final (2m: exact in f16)
+      acc[tw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(haw, hb, acc[tw], 0, 0, 0);
+      acc[tw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(haw, mb + mb, acc[tw], 0, 0, 0);
+    } else {
+      acc[tw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(haw, hb, acc[tw], 0, 0, 0);
+      acc[tw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(haw, mb, acc[tw], 0, 0, 0);
+      acc[tw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(maw, hb, acc[tw], 0, 0, 0);
+    }
     if constexpr (KT > 1 && B >= KT - 1 - W) {
       constexpr int to = O::slot_o(B);
-      acc[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(hao, hb, acc[to], 0, 0, 0);
-      acc[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(hao, mb, acc[to], 0, 0, 0);
-      acc[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(mao, hb, acc[to], 0, 0, 0);
+      if constexpr (GMK_H16_DIAG && B == KT - 1 - W) {
+        acc[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(hao, hb, acc[to], 0, 0, 0);
+        acc[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(hao, mb + mb, acc[to], 0, 0, 0);
+      } else {
+        acc[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(hao, hb, acc[to], 0, 0, 0);
+        acc[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(hao, mb, acc[to], 0, 0, 0);
+        acc[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(mao, hb, acc[to], 0, 0, 0);
+      }
     }
     h16_step_b<KT, W, B - 1>(Lh, Lm, off, haw, maw, hao, mao, acc);
   }
@@ -609,19 +637,20 @@ __device__ __forceinline__ void h16_step(const _Float16* Lh, const _Float16* Lm,
 // need (the compiler spilled 50-300 VGPRs at every unroll >= 3 tried).
 constexpr int kH16Sets = 2;
 
-template <int KT, int DBG, bool PANEL>
+template <int KT, int DBG, int WS>
 __device__ __forceinline__ void h16_producer(const float* __restrict__ X, int64_t K, int64_t ldx,
-                                             int64_t pstride, int wshift,
+                                             int64_t pstride,
                                              const float* __restrict__ p, int64_t c_begin,
                                              int64_t c_end, int nstage, H16Lds<KT>& lds,
                                              int* s_exp, float* s_bmax) {
   constexpr int RPT = GramShape<KT>::ROWS_PER_THREAD;
-  H16Stream<KT, kH16Sets, PANEL> P;
+  using Str = H16Stream<KT, kH16Sets, WS>;
+  Str P;
   const int t = threadIdx.x - 256;
   P.X = X; P.p = p; P.K = K; P.ldx = ldx; P.c_begin = c_begin; P.c_end = c_end;
-  P.pstride = pstride; P.wshift = wshift;
+  P.pstride = pstride;
   P.r0 = t >> 4; P.cg = t & 15;
-  P.voff = (uint32_t)P.r0 * (uint32_t)(pstride ? (1 << wshift) : ldx) * 4u;
+  P.voff = WS ? (uint32_t)(P.r0 * Str::RUN) << (WS + 2) : (uint32_t)P.r0 * (uint32_t)ldx * 4u;
   if (nstage == 0 || DBG == 2) {                 // no columns: meet the consumers' barriers
     if (DBG == 2)
       for (int k = t; k < GramShape<KT>::KP; k += 256) s_exp[k] = 0;
@@ -641,7 +670,7 @@ __device__ __forceinline__ void h16_producer(const float* __restrict__ X, int64_
   float mx = 0.f;
 #pragma unroll
   for (int i = 0; i < RPT; ++i)
-    if (P.r0 + 16 * i < K) mx = fmaxf(mx, fmaxf(P.template absmax<0>(i), P.template absmax<1>(i)));
+    if (P.row(i) < K) mx = fmaxf(mx, fmaxf(P.template absmax<0>(i), P.template absmax<1>(i)));
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
   if ((t & 63) == 0) s_bmax[t >> 6] = mx;
@@ -723,10 +752,9 @@ __device__ __forceinline__ void h16_consumer(int nstage, int nseg, float* __rest
     for (; seg < nseg; ++seg) flush(seg, true);              // blocks with fewer stages
 }
 
-template <int KT, int DBG, bool PANEL>
+template <int KT, int DBG, int WS>
 __global__ void __launch_bounds__(512, 1) gram_h16_partial(const float* __restrict__ X, int64_t K,
                                                            int64_t d, int64_t ldx, int64_t pstride,
-                                                           int wshift,
                                                            const float* __restrict__ p,
                                                            int64_t cols_per_block, int nseg,
                                                            float* __restrict__ slab) {
@@ -738,8 +766,7 @@ __global__ void __launch_bounds__(512, 1) gram_h16_partial(const float* __restri
   const int64_t c_end = c_begin + cols_per_block < d ? c_begin + cols_per_block : d;
   const int nstage = c_begin < c_end ? (int)((c_end - c_begin + kH16BK - 1) / kH16BK) : 0;
   if (w >= 4) {
-    h16_producer<KT, DBG, PANEL>(X, K, ldx, pstride, wshift, p, c_begin, c_end, nstage, lds, s_exp,
-                          s_bmax);
+    h16_producer<KT, DBG, WS>(X, K, ldx, pstride, p, c_begin, c_end, nstage, lds, s_exp, s_bmax);
     return;
   }
   if constexpr (KT == 8) {
@@ -784,9 +811,11 @@ __global__ void __launch_bounds__(256) gram_reduce_part(const float* __restrict_
   tmp[(int64_t)y * n + e] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
+// symdiag: the diagonal tiles hold hh^T + 2 h m^T (the f16 kernel): G takes their
+// symmetric part, (s(r,c) + s(c,r)) / 2, the same value at both positions.
 __global__ void __launch_bounds__(256) gram_reduce_final(const double* __restrict__ tmp, int NG,
                                                          int KT, double* __restrict__ G,
-                                                         KState* st) {
+                                                         KState* st, int symdiag) {
   const int tiles = KT * (KT + 1) / 2;
   const int64_t n = (int64_t)tiles * 1024;
   const int KP = 32 * KT;
@@ -801,8 +830,18 @@ __global__ void __launch_bounds__(256) gram_reduce_final(const double* __restric
     while (tri_index(a, KT - 1, KT) < tix) ++a;        // row tile of this triangle index
     const int bt = a + (tix - tri_index(a, a, KT));
     const int reg = el >> 6, ln = el & 63;
-    const int row = a * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (ln >> 5);
-    const int col = bt * 32 + (ln & 31);
+    const int ri = (reg & 3) + 8 * (reg >> 2) + 4 * (ln >> 5), ci = ln & 31;
+    const int row = a * 32 + ri;
+    const int col = bt * 32 + ci;
+    if (symdiag && a == bt && ri != ci) {
+      // the element at (ci, ri) of the same tile: lane ri + 32 * ((ci >> 2) & 1),
+      // register (ci & 3) + 4 * (ci >> 3)
+      const int64_t eT = ((int64_t)tix << 10) + (((ci & 3) + 4 * (ci >> 3)) << 6) + ri + 32 * ((ci >> 2) & 1);
+      double sT = 0.0;
+      for (int y = 0; y < NG; ++y) sT += tmp[(int64_t)y * n + eT];
+      bad |= !isfinite(sT);
+      s = 0.5 * (s + sT);                      // the same value at both positions
+    }
     G[(int64_t)row * KP + col] = s;
     G[(int64_t)col * KP + row] = s;
   }
@@ -968,15 +1007,20 @@ static hipError_t launch_split_kt(const float* X, int64_t K, int64_t d, int64_t 
 }
 
 template <int KT, int DBG>
-static void launch_h16_dbg(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t pstride,
-                           int wshift, const float* p, int nb, int64_t cpb, int nseg, float* slab,
-                           hipStream_t s) {
-  if (pstride)
-    hipLaunchKernelGGL((gram_h16_partial<KT, DBG, true>), dim3(nb), dim3(512), 0, s, X, K, d, ldx,
-                       pstride, wshift, p, cpb, nseg, slab);
-  else
-    hipLaunchKernelGGL((gram_h16_partial<KT, DBG, false>), dim3(nb), dim3(512), 0, s, X, K, d, ldx,
-                       pstride, wshift, p, cpb, nseg, slab);
+static hipError_t launch_h16_dbg(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t pstride,
+                                 int wshift, const float* p, int nb, int64_t cpb, int nseg,
+                                 float* slab, hipStream_t s) {
+  // panel widths of the Gram tiles (gm_panel_width at K <= 256): 64, 128, 256
+#define GMK_H16_LAUNCH(WS_)                                                                  \
+  hipLaunchKernelGGL((gram_h16_partial<KT, DBG, WS_>), dim3(nb), dim3(512), 0, s, X, K, d, ldx, \
+                     pstride, p, cpb, nseg, slab)
+  if (!pstride) GMK_H16_LAUNCH(0);
+  else if (wshift == 7) GMK_H16_LAUNCH(7);
+  else if (wshift == 6) GMK_H16_LAUNCH(6);
+  else if (wshift == 8) GMK_H16_LAUNCH(8);
+  else return hipErrorInvalidValue;
+#undef GMK_H16_LAUNCH
+  return hipSuccess;
 }
 
 template <int KT>
@@ -985,13 +1029,14 @@ static hipError_t launch_h16_kt(const float* X, int64_t K, int64_t d, int64_t ld
                                 float* slab, hipStream_t s) {
   // GMAGG_GRAM_DEBUG = 1 / 2: timing probes without MFMAs / without loads (wrong G)
   static const int dbg = [] { const char* e = getenv("GMAGG_GRAM_DEBUG"); return e ? atoi(e) : 0; }();
-  if (dbg == 1)
-    launch_h16_dbg<KT, 1>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, s);
-  else if (dbg == 2)
-    launch_h16_dbg<KT, 2>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, s);
+  hipError_t e;
+  if (KT == 8 && dbg == 1)   // probes built for the 256-row tile only
+    e = launch_h16_dbg<KT, KT == 8 ? 1 : 0>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, s);
+  else if (KT == 8 && dbg == 2)
+    e = launch_h16_dbg<KT, KT == 8 ? 2 : 0>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, s);
   else
-    launch_h16_dbg<KT, 0>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, s);
-  return hipGetLastError();
+    e = launch_h16_dbg<KT, 0>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, s);
+  return e != hipSuccess ? e : hipGetLastError();
 }
 
 // Grid of one Gram launch: blocks, columns per block, fp32 partials per block.
@@ -1056,7 +1101,7 @@ hipError_t launch_gram(const float* X, int64_t K, int64_t d, int64_t ldx, const 
   hipLaunchKernelGGL(gram_reduce_part, dim3((unsigned)((n + 255) / 256), ng), dim3(256), 0, s,
                      slab, parts, n, tmp);
   hipLaunchKernelGGL(gram_reduce_final, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tmp,
-                     ng, KT, G, st);
+                     ng, KT, G, st, (int)(kind == GramKind::H16 && GMK_H16_DIAG));
   return hipGetLastError();
 }
 
