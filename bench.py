@@ -138,7 +138,8 @@ def pmc_traffic(workload, layout, kernel="weiszfeld_pass", mode="0"):
                     return row["hbm_bytes_per_launch"] / 1e9, os.path.relpath(path, ROOT)
             elif kernel == "gram_h16_partial":
                 m = re.search(r"gram_h16_partial<([^>]*)>", name)
-                if m and m.group(1).split(", ")[-1] == ("true" if layout == "panels" else "false"):
+                # <KT, DBG, WS>: WS = log2 of the panel width, 0 for row-major X
+                if m and (m.group(1).split(", ")[-1] != "0") == (layout == "panels"):
                     return row["hbm_bytes_per_launch"] / 1e9, os.path.relpath(path, ROOT)
             elif kernel in name:
                 return row["hbm_bytes_per_launch"] / 1e9, os.path.relpath(path, ROOT)
