@@ -162,40 +162,190 @@ __device__ __forceinline__ float key_value(uint32_t k) {
 }
 
 // NC columns x NR ranks selected together: independent chains interleaved, so the
-// compare -> popcount -> decide latency of one chain hides behind the others.
-template <int R, int NC, int NR>
-__device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const int64_t (&r)[NR],
-                                             uint32_t (&ans)[NC][NR]) {
-#pragma unroll
-  for (int c = 0; c < NC; ++c)
-#pragma unroll
-    for (int q = 0; q < NR; ++q) ans[c][q] = 0;
-  // counts fit 32 bits (K <= 2048): one scalar add per ballot instead of a 64-bit pair
-  int rr[NR];
-#pragma unroll
-  for (int q = 0; q < NR; ++q) rr[q] = (int)r[q];
-  for (int bit = 31; bit >= 0; --bit) {
+// compare -> count -> decide latency of one chain hides behind the others.
+// count(t, cnt): cnt[c][q] = #(keys of chain (c, q) < t[c][q]), wave-uniform.
+template <int NC, int NR, typename Count>
+__device__ __forceinline__ void select_steps(int hi, int lo, uint32_t (&ans)[NC][NR],
+                                             int (&clo)[NC][NR], int (&chi)[NC][NR],
+                                             const int (&rr)[NR], Count count) {
+  for (int bit = hi; bit >= lo; --bit) {
+    uint32_t t[NC][NR];
     int cnt[NC][NR];
 #pragma unroll
     for (int c = 0; c < NC; ++c)
 #pragma unroll
-      for (int q = 0; q < NR; ++q) {
-        const uint32_t t = ans[c][q] | (1u << bit);
-        int n = 0;
-#pragma unroll
-        for (int i = 0; i < R; ++i) n += __popcll(__ballot(key[c][i] < t));
-        cnt[c][q] = n;
-      }
+      for (int q = 0; q < NR; ++q) t[c][q] = ans[c][q] | (1u << bit);
+    count(t, cnt);
 #pragma unroll
     for (int c = 0; c < NC; ++c)
 #pragma unroll
-      for (int q = 0; q < NR; ++q)
-        if (cnt[c][q] <= rr[q]) ans[c][q] |= 1u << bit;
+      for (int q = 0; q < NR; ++q) {
+        if (cnt[c][q] <= rr[q]) {
+          ans[c][q] |= 1u << bit;
+          clo[c][q] = cnt[c][q];
+        } else {
+          chi[c][q] = cnt[c][q];
+        }
+      }
   }
 }
 
-template <int R, int C>
-__global__ void __launch_bounds__(256) col_select(const float* __restrict__ X, int64_t K,
+// Sum over the wave of a per-lane int (DPP row shifts + row broadcasts, gfx9
+// family), returned wave-uniform.
+__device__ __forceinline__ int wave_sum_i32(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
+// Candidate compaction (round 2).  Before step `bit` a chain's answer lies in
+// [L, L + 2^(bit+1)); the step's count n = #(key < L + 2^bit) is also the count
+// below one end of the new interval, so the number of keys still in it (chi - clo)
+// is known for free.  At two fixed points of the schedule (after bits 31..24, and
+// after 23..16) the chains check it: if every chain has <= 64*R2 keys left, each
+// writes those keys (a ballot + mbcnt per held value) to LDS, reads back R2 per lane,
+// and the remaining steps count only them: n = c0 + #(candidate < t), c0 = the
+// count below L at compaction (every dropped key is below that L or at/above the
+// interval's end).  Spread data (the C3 recipe, N(0,1)) compacts after the first 8
+// steps (simulated: <= 128 of 1000 keys left after ~7); clustered data after 16 or
+// never, and then the loop counts every key as before.  The schedule is fixed and
+// branch-free inside each run of steps: a per-step compaction check cost more than
+// it saved.  buf(c, q): LDS slots of chain (c, q), STR words apart, >= 64*R2 of them.
+template <int R, int NC, int NR, int R2, int STR, typename Buf>
+__device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const int64_t (&r)[NR],
+                                             uint32_t (&ans)[NC][NR], Buf buf) {
+  constexpr bool COMPACT = R2 > 0 && R > R2;
+  int clo[NC][NR], chi[NC][NR];
+  int rr[NR];
+#pragma unroll
+  for (int q = 0; q < NR; ++q) rr[q] = (int)r[q];   // counts fit 32 bits (K <= 2048)
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      ans[c][q] = 0;
+      clo[c][q] = 0;
+      chi[c][q] = 64 * R;      // padding keys (0xFFFFFFFF) count as keys: never below t
+    }
+  // Counting every held key.  A ballot costs three instructions per key (v_cmp, a
+  // scalar popcount, a scalar add) and the loop is issue-bound (one instruction per
+  // wave per cycle slot), so at R >= 8 each lane counts its own keys instead (v_cmp +
+  // v_addc: two) and two chains share one DPP wave sum (16-bit halves: <= 2048 each).
+  auto full = [&](const uint32_t (&t)[NC][NR], int (&cnt)[NC][NR]) {
+    if constexpr (R >= 8 && (NC * NR) % 2 == 0) {
+      int lc[NC * NR];
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+          int v = 0;
+#pragma unroll
+          for (int i = 0; i < R; ++i) v += (int)(key[c][i] < t[c][q]);
+          lc[c * NR + q] = v;
+        }
+#pragma unroll
+      for (int p = 0; p < NC * NR; p += 2) {
+        const int s2 = wave_sum_i32(lc[p] + (lc[p + 1] << 16));
+        cnt[p / NR][p % NR] = s2 & 0xFFFF;
+        cnt[(p + 1) / NR][(p + 1) % NR] = s2 >> 16;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+          int n = 0;
+#pragma unroll
+          for (int i = 0; i < R; ++i) n += __popcll(__ballot(key[c][i] < t[c][q]));
+          cnt[c][q] = n;
+        }
+    }
+  };
+  if constexpr (!COMPACT) {
+    select_steps<NC, NR>(31, 0, ans, clo, chi, rr, full);
+  } else {
+    const int lane = threadIdx.x & 63;
+    auto small = [&]() {
+      bool ok = true;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int q = 0; q < NR; ++q) ok = ok && chi[c][q] - clo[c][q] <= 64 * R2;
+      return ok;
+    };
+    // keys in [ans, ans + 2^bit) of every chain -> LDS (lane order) -> R2 per lane,
+    // then steps bit-1 .. 0 on them
+    auto finish_compacted = [&](int bit) {
+      uint32_t ck[NC][NR][R2];
+      int cbase[NC][NR];
+      const uint32_t span = 1u << bit;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+          uint32_t* b = buf(c, q);
+          const uint32_t lo = ans[c][q];
+          int base = 0;
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            const bool in = key[c][i] - lo < span;
+            const uint64_t m = __ballot(in);
+            const int pos = base + (int)__builtin_amdgcn_mbcnt_hi(
+                                       (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (in) b[pos * STR] = key[c][i];
+            base += __popcll(m);
+          }
+          cbase[c][q] = clo[c][q];
+        }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+          const uint32_t* b = buf(c, q);
+          const int nc = chi[c][q] - clo[c][q];
+#pragma unroll
+          for (int i = 0; i < R2; ++i) {
+            const int s = lane + 64 * i;
+            ck[c][q][i] = s < nc ? b[s * STR] : 0xFFFFFFFFu;
+          }
+        }
+      select_steps<NC, NR>(bit - 1, 0, ans, clo, chi, rr,
+                           [&](const uint32_t (&t)[NC][NR], int (&cnt)[NC][NR]) {
+#pragma unroll
+                             for (int c = 0; c < NC; ++c)
+#pragma unroll
+                               for (int q = 0; q < NR; ++q) {
+                                 int n = cbase[c][q];
+#pragma unroll
+                                 for (int i = 0; i < R2; ++i)
+                                   n += __popcll(__ballot(ck[c][q][i] < t[c][q]));
+                                 cnt[c][q] = n;
+                               }
+                           });
+    };
+    select_steps<NC, NR>(31, 24, ans, clo, chi, rr, full);
+    if (small()) {
+      finish_compacted(24);
+      return;
+    }
+    select_steps<NC, NR>(23, 16, ans, clo, chi, rr, full);
+    if (small()) {
+      finish_compacted(16);
+      return;
+    }
+    select_steps<NC, NR>(15, 0, ans, clo, chi, rr, full);
+  }
+}
+
+template <int R, int C, int NWV>
+__global__ void __launch_bounds__(NWV * 64) col_select(const float* __restrict__ X, int64_t K,
                                                   int64_t d, int64_t ldx, int mode, int64_t b,
                                                   int vec4, float* __restrict__ out) {
   __shared__ float tile[64 * R][C + 1];
@@ -208,7 +358,7 @@ __global__ void __launch_bounds__(256) col_select(const float* __restrict__ X, i
   {
     // float4 per lane (LPR lanes per row segment), 16 loads in flight per thread
     typedef float f4 __attribute__((ext_vector_type(4)));
-    constexpr int LPR = C / 4, RPI = 256 / LPR;
+    constexpr int LPR = C / 4, RPI = NWV * 64 / LPR;
     const int tq = threadIdx.x % LPR, tr = threadIdx.x / LPR;
     const int64_t col = j0 + 4 * tq;
     const bool vec = vec4 && col + 4 <= d;
@@ -239,9 +389,10 @@ __global__ void __launch_bounds__(256) col_select(const float* __restrict__ X, i
     }
   }
   __syncthreads();
-  // wave w selects columns w, w+4, ... in pairs (w + 8m, w + 8m + 4): C % 8 == 0
+  // wave w selects columns in pairs (w + 2m NWV, w + 2m NWV + NWV): C % (2 NWV) == 0
+  static_assert(C % (2 * NWV) == 0, "column pairs");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int c0 = w; c0 < C; c0 += 8) {
+  for (int c0 = w; c0 < C; c0 += 2 * NWV) {
     if (j0 + c0 >= d) break;
     uint32_t key[2][R];      // values are recovered from keys (key_value) when summed
     bool nan[2] = {false, false};
@@ -250,23 +401,29 @@ __global__ void __launch_bounds__(256) col_select(const float* __restrict__ X, i
 #pragma unroll
       for (int i = 0; i < R; ++i) {
         const int row = lane + 64 * i;
-        const bool ok = row < K && j0 + c0 + 4 * h < d;
-        const float x = ok ? tile[row][c0 + 4 * h] : 0.f;
+        const bool ok = row < K && j0 + c0 + NWV * h < d;
+        const float x = ok ? tile[row][c0 + NWV * h] : 0.f;
         key[h][i] = ok ? order_key(x) : 0xFFFFFFFFu;
         nan[h] |= ok && x != x;
       }
     float res[2];
+    // compaction slots of chain (h, q): column c0 + NWV h of the tile (this wave's own
+    // column, dead once its keys are in registers), rows from q * 64 * R2
+    constexpr int R2 = R >= 4 ? 2 : 0;
+    auto buf = [&](int h, int q) {
+      return reinterpret_cast<uint32_t*>(&tile[q * 64 * (R2 > 0 ? R2 : 1)][c0 + NWV * h]);
+    };
     if (mode == 0) {
       const int64_t rk[1] = {(K - 1) / 2};
       uint32_t ans[2][1];
-      select_ranks<R, 2, 1>(key, rk, ans);
+      select_ranks<R, 2, 1, R2, C + 1>(key, rk, ans, buf);
 #pragma unroll
       for (int h = 0; h < 2; ++h)
         res[h] = __ballot(nan[h]) ? __uint_as_float(0x7FC00000u) : key_value(ans[h][0]);
     } else {
       const int64_t rk[2] = {b, K - b - 1};
       uint32_t ans[2][2];
-      select_ranks<R, 2, 2>(key, rk, ans);
+      select_ranks<R, 2, 2, R2, C + 1>(key, rk, ans, buf);
       const int64_t n = K - 2 * b;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -293,7 +450,7 @@ __global__ void __launch_bounds__(256) col_select(const float* __restrict__ X, i
     }
     if (lane == 0) {
       out[j0 + c0] = res[0];
-      if (j0 + c0 + 4 < d) out[j0 + c0 + 4] = res[1];
+      if (j0 + c0 + NWV < d) out[j0 + c0 + NWV] = res[1];
     }
   }
 }
@@ -493,15 +650,17 @@ hipError_t launch_col_mean(const float* X, int64_t K, int64_t d, int64_t ldx, fl
 hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, int mode,
                              int64_t b, float* out, hipStream_t s) {
   const int vec4 = reinterpret_cast<uintptr_t>(X) % 16 == 0 && ldx % 4 == 0;
-#define GMK_SEL(R, C)                                                                       \
-  hipLaunchKernelGGL((col_select<R, C>), dim3((unsigned)((d + C - 1) / C)), dim3(256), 0, s, X, K, \
-                     d, ldx, mode, b, vec4, out)
-  if (K <= 64) GMK_SEL(1, 32);
-  else if (K <= 128) GMK_SEL(2, 32);
-  else if (K <= 256) GMK_SEL(4, 32);
-  else if (K <= 512) GMK_SEL(8, 16);
-  else if (K <= 1024) GMK_SEL(16, 16);
-  else if (K <= 2048) GMK_SEL(32, 8);
+#define GMK_SEL(R, C, NWV)                                                                    \
+  hipLaunchKernelGGL((col_select<R, C, NWV>), dim3((unsigned)((d + C - 1) / C)), dim3(NWV * 64), 0, \
+                     s, X, K, d, ldx, mode, b, vec4, out)
+  // K <= 1024: 8 waves per 69.6-KB tile (one column pair each) so that the CU holds
+  // 4 waves per SIMD (the LDS allows 2 tiles) instead of 2
+  if (K <= 64) GMK_SEL(1, 32, 4);
+  else if (K <= 128) GMK_SEL(2, 32, 4);
+  else if (K <= 256) GMK_SEL(4, 32, 4);
+  else if (K <= 512) GMK_SEL(8, 16, 4);
+  else if (K <= 1024) GMK_SEL(16, 16, 8);
+  else if (K <= 2048) GMK_SEL(32, 8, 4);
   else return hipErrorInvalidValue;
 #undef GMK_SEL
   return hipGetLastError();
