@@ -164,10 +164,12 @@ __device__ __forceinline__ float key_value(uint32_t k) {
 // NC columns x NR ranks selected together: independent chains interleaved, so the
 // compare -> count -> decide latency of one chain hides behind the others.
 // count(t, cnt): cnt[c][q] = #(keys of chain (c, q) < t[c][q]), wave-uniform.
-template <int NC, int NR, typename Count>
-__device__ __forceinline__ void select_steps(int hi, int lo, uint32_t (&ans)[NC][NR],
-                                             int (&clo)[NC][NR], int (&chi)[NC][NR],
-                                             const int (&rr)[NR], Count count) {
+// EXIT: stop as soon as every chain's interval holds a single key (returns the bit
+// just decided: that key is the answer); -1 when the steps ran to `lo`.
+template <int NC, int NR, bool EXIT = false, typename Count>
+__device__ __forceinline__ int select_steps(int hi, int lo, uint32_t (&ans)[NC][NR],
+                                            int (&clo)[NC][NR], int (&chi)[NC][NR],
+                                            const int (&rr)[NR], Count count) {
   for (int bit = hi; bit >= lo; --bit) {
     uint32_t t[NC][NR];
     int cnt[NC][NR];
@@ -187,7 +189,16 @@ __device__ __forceinline__ void select_steps(int hi, int lo, uint32_t (&ans)[NC]
           chi[c][q] = cnt[c][q];
         }
       }
+    if constexpr (EXIT) {
+      bool one = true;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int q = 0; q < NR; ++q) one = one && chi[c][q] - clo[c][q] == 1;
+      if (one) return bit;
+    }
   }
+  return -1;
 }
 
 // Sum over the wave of a per-lane int (DPP row shifts + row broadcasts, gfx9
@@ -316,7 +327,10 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
             ck[c][q][i] = s < nc ? b[s * STR] : 0xFFFFFFFFu;
           }
         }
-      select_steps<NC, NR>(bit - 1, 0, ans, clo, chi, rr,
+      // a chain whose interval holds one candidate has found its key (simulated: one
+      // key left after 13-18 of the 32 steps on spread data), so the steps stop
+      // when every chain is there and each takes that key
+      const int stop = select_steps<NC, NR, true>(bit - 1, 0, ans, clo, chi, rr,
                            [&](const uint32_t (&t)[NC][NR], int (&cnt)[NC][NR]) {
 #pragma unroll
                              for (int c = 0; c < NC; ++c)
@@ -329,6 +343,21 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
                                  cnt[c][q] = n;
                                }
                            });
+      if (stop > 0) {
+        const uint32_t sp = 1u << stop;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int q = 0; q < NR; ++q) {
+            uint32_t v = ans[c][q];
+#pragma unroll
+            for (int i = 0; i < R2; ++i) {
+              const uint64_t m = __ballot(ck[c][q][i] - ans[c][q] < sp);
+              if (m) v = __builtin_amdgcn_readlane(ck[c][q][i], __builtin_ctzll(m));
+            }
+            ans[c][q] = v;
+          }
+      }
     };
     select_steps<NC, NR>(31, 24, ans, clo, chi, rr, full);
     if (small()) {
