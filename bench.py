@@ -76,6 +76,9 @@ def parse():
                         "is timed too (alt_layout in the JSON line).")
     p.add_argument("--alt-steps", type=int, default=None,
                    help="steps for the other layout's measurement (0 = skip)")
+    p.add_argument("--soak", type=float, default=8.0,
+                   help="seconds of untimed aggregations after the timed region (0 = none): the "
+                        "GPU stays busy long enough for an outside utilisation sampler to see it")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-d", type=int, default=2_000_000, help="CPU sample width (columns)")
     p.add_argument("--cpu-budget", type=float, default=20.0,
@@ -481,6 +484,17 @@ def main():
 
     elapsed, pass_ms, launches, res, out = measure(inputs(layout), args.steps, args.warmup)
     passes = 2 if res.algo.startswith("gram") else res.iters + 1
+    # untimed soak: the same aggregation repeated for ~args.soak seconds (a count every
+    # rank derives from the max-over-ranks time, so collectives stay in lockstep)
+    soak = None
+    if args.soak > 0:
+        n_soak = int(args.soak / max(elapsed / args.steps, 1e-6))
+        t0 = time.perf_counter()
+        for _ in range(n_soak):
+            agg(inputs(layout), opts)
+        torch.cuda.synchronize(dev)
+        soak = {"aggregations": n_soak, "seconds": time.perf_counter() - t0,
+                "note": "untimed, after the timed region (GPU-busy signal for outside samplers)"}
     alt = None
     alt_layout = "rows" if layout == "panels" else "panels"
     alt_steps = args.alt_steps if args.alt_steps is not None else max(3, args.steps // 4)
@@ -612,6 +626,7 @@ def main():
             "cpu_baseline": None,
             "check": check,
             "alt_layout": alt,
+            "soak": soak,
         }
         if world == 1 and not args.no_cpu and not args.rehearse_shard:
             line["cpu_baseline"] = cpu_baseline(X, g0, agg_name, var, res.iters, d_total,

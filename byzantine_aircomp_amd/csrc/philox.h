@@ -33,7 +33,15 @@ __host__ __device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t
     uint32_t hi0, hi1;
     uint32_t lo0 = mulhilo(0xD2511F53u, c.x, &hi0);
     uint32_t lo1 = mulhilo(0xCD9E8D57u, c.z, &hi1);
+#ifdef __HIP_DEVICE_COMPILE__
+    // gfx950's three-input bitwise op (truth table 0x96 = a ^ b ^ c): one VALU
+    // instruction per word instead of two v_xor_b32 (the compiler selects no bitop3
+    // for a ^ b ^ c itself); the same bits
+    c = u4{(uint32_t)__builtin_amdgcn_bitop3_b32(hi1, c.y, k0, 0x96), lo1,
+           (uint32_t)__builtin_amdgcn_bitop3_b32(hi0, c.w, k1, 0x96), lo0};
+#else
     c = u4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+#endif
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
