@@ -184,13 +184,17 @@ int allreduce(gm_ctx* c, double* buf, int64_t n, hipStream_t s) {
 // The tile is K_pad x J with J = LPR*V columns; NRG = 16*64/LPR row groups of
 // R rows each cover K.  Bigger K -> narrower chunk, so a block's tile (and the
 // bytes it has in flight) stays ~64-128 KiB.
-bool pick_cfg(int64_t K, int V, int64_t ldx, PassCfg* cfg) {
+// panel: the tile of a panel-layout call (its chunk width is the panel width W).
+bool pick_cfg(int64_t K, int V, int64_t ldx, PassCfg* cfg, bool panel = false) {
   int nw = 16, lpr, r, occ = 1;
   if (K <= 16) { lpr = 64; r = 1; }
   else if (K <= 32) { lpr = 64; r = 2; }
   else if (K <= 64) { lpr = 64; r = 4; }
   else if (K <= 128) { lpr = 64; r = 8; }
-  else if (K <= 256) { lpr = 32; r = 8; }
+  // 128 < K <= 256 on panels: 256 x 64 chunks (W = 64, each chunk 64 KB contiguous),
+  // STEP 2.38 vs 2.54 ms and the C4-shard Gram closing pass 2.58 vs 2.80 ms against the
+  // 256 x 128 tile (profiles/r2_k256_tiles.txt); rows keep the 512-B row segments
+  else if (K <= 256) { if (panel) { lpr = 16; r = 4; } else { lpr = 32; r = 8; } }
   else if (K <= 512) { lpr = 16; r = 8; }
   // K <= 1024: two 512-thread blocks per CU, each with a 1024 x 32 tile (128 B row
   // segments): 6.29 vs 6.05 TB/s for one 1024-thread block (profiles/r01_occ_sweep.txt)
@@ -439,7 +443,7 @@ int gm_abi_version(void) { return GMAGG_ABI_VERSION; }
 
 int64_t gm_panel_width(int64_t K) {
   PassCfg cfg{};
-  return K >= 1 && pick_cfg(K, 4, 1, &cfg) ? (int64_t)cfg.LPR * cfg.V : 0;
+  return K >= 1 && pick_cfg(K, 4, 1, &cfg, true) ? (int64_t)cfg.LPR * cfg.V : 0;
 }
 
 int gm_ctx_create(int device, gm_ctx** out) {
@@ -574,7 +578,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
     // [ceil(d/W)][K][W] panels: the streaming pass only, with the tile whose chunk
     // width is W (pick_cfg's tile for K; light_cfg's wider INIT tile is not used).
     const int64_t W = gm_panel_width(K);
-    if (W == 0 || !pick_cfg(K, 4, W, &cfg) || cfg.LPR * cfg.V != W)
+    if (W == 0 || !pick_cfg(K, 4, W, &cfg, true) || cfg.LPR * cfg.V != W)
       return fail(GM_ERR_UNSUPPORTED, "panel layout: no streaming tile of width %lld for K=%lld",
                   (long long)W, (long long)K);
     if (ldx < K * W || (reinterpret_cast<uintptr_t>(X) & 15) || K * W * 4 > 0x7fffffff)
@@ -606,7 +610,9 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   // Sharded: the choice is made on d_total (every rank the same); each rank's
   // shard must then meet the kernel's local needs, which shard_range-aligned,
   // contiguous shards of a d_total % 4 == 0 update always do.
-  const bool gram_local_ok = gram_kt(K) > 0 && V == 4 && ldx < ((int64_t)1 << 26) &&
+  // (panels never take this path, and their tile in cfg must stay: it sets the chunk
+  // width the panel layout was built for)
+  const bool gram_local_ok = !panels && gram_kt(K) > 0 && V == 4 && ldx < ((int64_t)1 << 26) &&
                              pick_cfg(K, V, ldx, &cfg);
   bool guard_rejected = panel_gram_rejected;   // a Gram result was computed and refused
   const bool gram_auto = algo == GM_ALGO_AUTO && o->mode == GM_MODE_IDEAL && !panels &&

@@ -33,8 +33,17 @@ def world1(request):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     kw = {"device_id": dev} if request.param == "nccl" else {}
-    dist.init_process_group(request.param, init_method=f"tcp://127.0.0.1:{_free_port()}",
-                            rank=0, world_size=1, **kw)
+    # a port found free can be taken by another socket before the store binds it
+    # (EADDRINUSE seen once on the box): take a fresh one then
+    for attempt in range(5):
+        try:
+            dist.init_process_group(request.param,
+                                    init_method=f"tcp://127.0.0.1:{_free_port()}",
+                                    rank=0, world_size=1, **kw)
+            break
+        except dist.DistNetworkError:
+            if attempt == 4:
+                raise
     try:
         yield request.param
     finally:
