@@ -227,15 +227,21 @@ def run_c5(args, json_out):
     stream = torch.cuda.current_stream(dev).cuda_stream
     per_var = args.problems // len(C5_VARS)
     chunk = min(1024, per_var)
-    groups = []                      # (var, X [P, K, d], g0 [P, d])
+    # layout: the batched problems in the panel layout (ProblemPanels: every chunk one
+    # contiguous block, as for C3) unless --layout rows; the panels are packed from the
+    # row-major fill, untimed
+    from byzantine_aircomp_amd.batched import ProblemPanels
+    use_panels = args.layout in ("auto", "panels")
+    groups = []                      # (var, X [P, K, d], g0 [P, d], panels or None)
     for vi, var in enumerate(C5_VARS):
         for c0 in range(0, per_var, chunk):
             P = min(chunk, per_var - c0)
             groups.append((vi, var, c0, torch.empty(P, K, d, device=dev),
-                           torch.empty(P, d, device=dev)))
+                           torch.empty(P, d, device=dev),
+                           ProblemPanels(P, K, d, device=dev) if use_panels else None))
 
     def fill():
-        for vi, var, c0, X, g0 in groups:
+        for vi, var, c0, X, g0, _ in groups:
             for p in range(X.shape[0]):
                 B = C5_BYZ[(c0 + p) % 3]
                 _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, X[p].data_ptr(), K, d, d, B, 0.0,
@@ -243,11 +249,15 @@ def run_c5(args, json_out):
                            "fill")
             _lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), g0.numel(), 0.0, 0.01,
                                                   777 + vi + c0, stream), "fill")
+        for *_, X, _g, Pn in groups:
+            if Pn is not None:
+                Pn.copy_rows_(X)
         torch.cuda.synchronize(dev)
 
     def step(reading):
         iters, per_group = [], {}
-        for vi, var, c0, X, g0 in groups:
+        for vi, var, c0, Xr, g0, Pn in groups:
+            X = Pn if Pn is not None else Xr
             opts = {"maxiter": args.maxiter, "tol": 1e-5, "guess": g0}
             t0 = time.perf_counter()
             if var == 0.0:
@@ -316,6 +326,7 @@ def run_c5(args, json_out):
                                   if args.reading == "prenoise" else " (AirComp gm for var > 0)"),
                    "K": K, "d": d, "problems": n_prob, "mean_iters": mean_it,
                    "parallelism": "batched (one launch per pass covers every problem of a group)",
+                   "layout": "panels (ProblemPanels)" if use_panels else "rows",
                    "groups": {str(k): {"problems_per_s": v["problems"] / v["seconds"],
                                        "mean_iters": v["iters"] / v["problems"]}
                               for k, v in per_group.items()}},

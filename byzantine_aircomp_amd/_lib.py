@@ -82,6 +82,8 @@ SIGNATURES = [
      [_P, _P, _I64, _I64, _I64, _I64, _I64, C.c_double, C.c_uint64, _P]),
     ("gm_oma_philox_panels_f32", C.c_int, [_P, _P, _I64, _I64, _I64, C.c_double, C.c_uint64,
                                             _P]),
+    ("gm_oma_philox_batched_panels_f32", C.c_int,
+     [_P, _P, _I64, _I64, _I64, _I64, _I64, C.c_double, C.c_uint64, _P]),
     ("gm_rows_to_panels_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _P, _I64, _I64, _P]),
     ("gm_oma_apply_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P]),
     ("gm_fill_clients_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _I64, C.c_float, C.c_float,

@@ -17,25 +17,89 @@ import torch
 
 from . import _lib
 from .aggregators import GMResult, _ALGO_NAMES, _seed, _stream_ptr, context
+from .panels import panel_width
 
-__all__ = ["gm2_batched", "gm_batched", "oma_batched", "SEED_STRIDE"]
+__all__ = ["gm2_batched", "gm_batched", "oma_batched", "ProblemPanels", "SEED_STRIDE"]
 
 SEED_STRIDE = 0x9E3779B97F4A7C15
 
 
-def _run(X: torch.Tensor, options: dict, aircomp: bool):
-    if X.dim() != 3:
-        raise ValueError(f"X must be [P, K, d] (got {tuple(X.shape)})")
-    if X.device.type != "cuda" or X.dtype != torch.float32:
-        raise TypeError("batched aggregation needs an fp32 CUDA tensor")
-    if X.stride(2) != 1 or X.stride(1) < X.shape[2] or X.stride(0) < X.shape[1] * X.stride(1):
-        X = X.contiguous()
-    P, K, d = X.shape
+class ProblemPanels:
+    """P independent client matrices (K x d each) in the panel layout: ``data[P, npan, K, W]``
+    (W = ``panel_width(K)``), each problem a ``ClientPanels``-layout block, so that every
+    streaming chunk of every problem is one contiguous block of HBM.  The batched calls
+    accept it in place of a ``[P, K, d]`` tensor; results are bit-identical to the
+    row-major batched call where both run the same tile (K outside 32 < K <= 64 and
+    128 < K <= 256, d % 4 == 0), equal to rounding otherwise."""
+
+    def __init__(self, P: int, K: int, d: int, device=None):
+        self.P, self.K, self.d = int(P), int(K), int(d)
+        self.W = panel_width(self.K)
+        self.npan = -(-self.d // self.W)
+        dev = torch.device(device) if device is not None else torch.device("cuda")
+        self.data = torch.zeros(self.P, self.npan, self.K, self.W, dtype=torch.float32, device=dev)
+
+    @property
+    def shape(self):
+        return torch.Size((self.P, self.K, self.d))
+
+    @property
+    def device(self):
+        return self.data.device
+
+    @property
+    def panel_stride(self) -> int:
+        return self.K * self.W
+
+    @property
+    def problem_stride(self) -> int:
+        return self.npan * self.K * self.W
+
+    def copy_rows_(self, X: torch.Tensor):
+        """Fill from row-major problems X [P, K, d] (on the device: one pack kernel each)."""
+        if tuple(X.shape) != (self.P, self.K, self.d):
+            raise ValueError(f"rows must be [{self.P}, {self.K}, {self.d}] (got {tuple(X.shape)})")
+        X = X.to(self.device, torch.float32)
+        if X.stride(2) != 1:
+            X = X.contiguous()
+        ctx = context(self.device)
+        with torch.cuda.device(self.device):
+            for p in range(self.P):
+                _lib.check(ctx.lib.gm_rows_to_panels_f32(
+                    ctx.handle, X[p].data_ptr(), self.K, self.d, X.stride(1),
+                    self.data[p].data_ptr(), self.W, self.panel_stride,
+                    _stream_ptr(self.device)), "gm_rows_to_panels_f32")
+        return self
+
+    @classmethod
+    def from_rows(cls, X: torch.Tensor):
+        P, K, d = X.shape
+        return cls(P, K, d, device=X.device).copy_rows_(X)
+
+    def to_rows(self) -> torch.Tensor:
+        full = self.data.permute(0, 2, 1, 3).reshape(self.P, self.K, self.npan * self.W)
+        return full[:, :, :self.d].contiguous()
+
+
+def _run(X, options: dict, aircomp: bool):
+    panels = isinstance(X, ProblemPanels)
+    if panels:
+        P, K, d = X.shape
+        buf, ldx, ldp = X.data, X.panel_stride, X.problem_stride
+    else:
+        if X.dim() != 3:
+            raise ValueError(f"X must be [P, K, d] (got {tuple(X.shape)})")
+        if X.device.type != "cuda" or X.dtype != torch.float32:
+            raise TypeError("batched aggregation needs an fp32 CUDA tensor")
+        if X.stride(2) != 1 or X.stride(1) < X.shape[2] or X.stride(0) < X.shape[1] * X.stride(1):
+            X = X.contiguous()
+        P, K, d = X.shape
+        buf, ldx, ldp = X, X.stride(1), X.stride(0)
     opts = {"maxiter": 200, "tol": 1e-5, "noise_var": None, "P_max": 1}
     opts.update(options or {})
     guess = opts.get("guess")
     if guess is None:
-        guess = X.mean(dim=1)
+        guess = (X.to_rows() if panels else X).mean(dim=1)
     g0 = guess.to(device=X.device, dtype=torch.float32).contiguous()
     if tuple(g0.shape) != (P, d):
         raise ValueError(f"guess must be [P, d] = [{P}, {d}]")
@@ -46,6 +110,7 @@ def _run(X: torch.Tensor, options: dict, aircomp: bool):
     o.eps = 1e-4
     o.mode = _lib.GM_MODE_AIRCOMP if aircomp else _lib.GM_MODE_IDEAL
     o.check_every = int(opts.get("check_every", 0))
+    o.layout = _lib.GM_LAYOUT_PANELS if panels else _lib.GM_LAYOUT_ROWS
     if aircomp:
         var = opts["noise_var"]
         o.has_noise = int(var is not None)
@@ -56,17 +121,26 @@ def _run(X: torch.Tensor, options: dict, aircomp: bool):
     ctx = context(X.device)
     with torch.cuda.device(X.device):
         _lib.check(ctx.lib.gm_weiszfeld_batched_f32(
-            ctx.handle, X.data_ptr(), P, K, d, X.stride(1), X.stride(0), g0.data_ptr(), d,
+            ctx.handle, buf.data_ptr(), P, K, d, ldx, ldp, g0.data_ptr(), d,
             out.data_ptr(), d, C.byref(o), res, _stream_ptr(X.device)), "gm_weiszfeld_batched_f32")
     results = [GMResult(r.iters, r.last_movement, bool(r.converged),
                         _ALGO_NAMES.get(r.algo_used, "?")) for r in res]
     return out, results
 
 
-def oma_batched(X: torch.Tensor, noise_var: float, seed: int = 2021) -> torch.Tensor:
-    """OMA pre-noise (M:385-394) in place on each of P problems X[p] ([P, K, d]):
-    the reference's `--agg gm2 --var v` path adds it before gm2 (M:351-352).
-    Problem p's draws equal `aggregators.OMA(X[p], noise_var, seed + p * SEED_STRIDE)`."""
+def oma_batched(X, noise_var: float, seed: int = 2021):
+    """OMA pre-noise (M:385-394) in place on each of P problems X[p] ([P, K, d] or
+    ProblemPanels): the reference's `--agg gm2 --var v` path adds it before gm2
+    (M:351-352).  Problem p's draws equal `aggregators.OMA(X[p], noise_var, seed + p *
+    SEED_STRIDE)`, in either layout."""
+    if isinstance(X, ProblemPanels):
+        ctx = context(X.device)
+        with torch.cuda.device(X.device):
+            _lib.check(ctx.lib.gm_oma_philox_batched_panels_f32(
+                ctx.handle, X.data.data_ptr(), X.P, X.K, X.d, X.panel_stride, X.problem_stride,
+                float(noise_var), int(seed) & 0xFFFFFFFFFFFFFFFF, _stream_ptr(X.device)),
+                "gm_oma_philox_batched_panels_f32")
+        return X
     if X.dim() != 3 or X.device.type != "cuda" or X.dtype != torch.float32 or X.stride(2) != 1:
         raise TypeError("oma_batched needs an fp32 CUDA [P, K, d] tensor with unit column stride")
     P, K, d = X.shape

@@ -189,7 +189,10 @@ bool pick_cfg(int64_t K, int V, int64_t ldx, PassCfg* cfg, bool panel = false) {
   int nw = 16, lpr, r, occ = 1;
   if (K <= 16) { lpr = 64; r = 1; }
   else if (K <= 32) { lpr = 64; r = 2; }
-  else if (K <= 64) { lpr = 64; r = 4; }
+  // 32 < K <= 64 on panels (C5's K = 50 batched problems): 512-thread blocks of 64 x 128
+  // chunks, 5.41-5.49 vs 5.07-5.13 TB/s per C5 STEP pass (profiles/r2_c5_panels.txt); rows
+  // keep (16,64,4), whose 256-column chunks let C1/C2 stay register-resident
+  else if (K <= 64) { if (panel) { nw = 8; lpr = 32; r = 4; } else { lpr = 64; r = 4; } }
   else if (K <= 128) { lpr = 64; r = 8; }
   // 128 < K <= 256 on panels: 256 x 64 chunks (W = 64, each chunk 64 KB contiguous),
   // STEP 2.38 vs 2.54 ms and the C4-shard Gram closing pass 2.58 vs 2.80 ms against the
@@ -873,10 +876,19 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
                              void* stream) {
   if (!c || !o || !X || !guess0 || !out)
     return fail(GM_ERR_INVALID, "gm_weiszfeld_batched_f32: NULL argument");
-  if (P < 1 || P > 65535 || K < 1 || d < 1 || ldx < d || ldp < K * ldx || ldg < d || ldo < d ||
-      o->maxiter < 0)
+  // GM_LAYOUT_PANELS: problem p is [ceil(d/W)][K][W] at X + p*ldp, ldx = its panel stride
+  const bool panels = o->layout == GM_LAYOUT_PANELS;
+  if (o->layout != GM_LAYOUT_ROWS && !panels)
+    return fail(GM_ERR_INVALID, "gm_weiszfeld_batched_f32: unknown layout %d", o->layout);
+  const int64_t Wp = panels ? gm_panel_width(K) : 0;
+  const int64_t rows_per_problem = panels ? (Wp > 0 ? (d + Wp - 1) / Wp : 0) : K;
+  if (P < 1 || P > 65535 || K < 1 || d < 1 || ldx < (panels ? K * Wp : d) ||
+      ldp < rows_per_problem * ldx || ldg < d || ldo < d || o->maxiter < 0 || (panels && Wp == 0))
     return fail(GM_ERR_INVALID, "gm_weiszfeld_batched_f32: bad shape P=%lld K=%lld d=%lld",
                 (long long)P, (long long)K, (long long)d);
+  if (panels && ((reinterpret_cast<uintptr_t>(X) & 15) || ldp % 4 || K * Wp * 4 > 0x7fffffff))
+    return fail(GM_ERR_INVALID, "gm_weiszfeld_batched_f32 (panels): 16-byte aligned X and "
+                "problem stride, K*W*4 < 2^31");
   if (o->mode == GM_MODE_AIRCOMP && o->noise_source != GM_NOISE_PHILOX)
     return fail(GM_ERR_UNSUPPORTED, "batched AirComp uses Philox noise only");
   if (c->d_total > 0) return fail(GM_ERR_UNSUPPORTED, "batched problems are not d-sharded");
@@ -891,14 +903,21 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
     return GM_OK;
   }
   PassCfg cfg{};
-  int V = pick_vec(X, d, ldx);
+  int V = panels ? 4 : pick_vec(X, d, ldx);
   if (ldp % V) V = 1;
-  if (!pick_cfg(K, V, ldx, &cfg))
+  if (!pick_cfg(K, V, ldx, &cfg, panels) || (panels && cfg.LPR * cfg.V != Wp))
     return fail(GM_ERR_UNSUPPORTED, "batched streaming pass supports K <= 2048");
   const int init_mode = o->mode == GM_MODE_AIRCOMP ? 2 : 1;
   const int J = cfg.LPR * cfg.V;
   const int64_t nch = (d + J - 1) / J;
-  const int64_t target = (int64_t)c->num_cu * pass_blocks_per_cu(cfg, 0) * 2;
+  // blocks per problem: the grid is OVERSUB rounds of co-resident blocks, so that the
+  // iterations where only the slowest problems are still active (the others exit at
+  // their `done` flag) still spread over the chip (GMAGG_BATCH_OVERSUB: A/B)
+  static const int oversub = [] {
+    const char* e = getenv("GMAGG_BATCH_OVERSUB");
+    return e && atoi(e) > 0 ? atoi(e) : 2;
+  }();
+  const int64_t target = (int64_t)c->num_cu * pass_blocks_per_cu(cfg, 0) * oversub;
   const int nbp = (int)std::max<int64_t>(1, std::min<int64_t>(nch, (target + P - 1) / P));
   const int64_t S = 2 * K + 2;
 
@@ -957,6 +976,7 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
     a.gnew_ps = d;
     a.coef = coef; a.st = st; a.slab = slab; a.slab_stride = init ? S : K + 2;
     a.noise = noise_kind; a.seed = o->seed; a.iter = t;
+    a.panel_stride = panels ? ldx : 0;
     hipEvent_t e0, e1;
     int rc2 = init ? GM_OK : record_pass_begin(c, s, &e0, &e1);
     if (rc2) return rc2;
@@ -978,7 +998,11 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
   ka.do_check = 0;
   ka.do_coef = 1;
   HIPCHK(launch_kspace(ka, s, (int)P));
-  int check_every = o->check_every > 0 ? o->check_every : 16;
+  static const int batch_check = [] {
+    const char* e = getenv("GMAGG_BATCH_CHECK");
+    return e && atoi(e) > 0 ? atoi(e) : 16;
+  }();
+  int check_every = o->check_every > 0 ? o->check_every : batch_check;
   for (int64_t t = 0; t < o->maxiter; ++t) {
     rc = do_pass(t);
     if (rc) return rc;
@@ -1118,6 +1142,24 @@ int gm_oma_philox_batched_f32(gm_ctx* c, float* X, int64_t P, int64_t K, int64_t
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(launch_oma_philox(X, K, d, ldx, d, 0, (float)std::sqrt(noise_var), seed,
                            reinterpret_cast<hipStream_t>(stream), 0, P, P > 1 ? pstride : 0));
+  return GM_OK;
+}
+
+int gm_oma_philox_batched_panels_f32(gm_ctx* c, float* X, int64_t P, int64_t K, int64_t d,
+                                     int64_t panel_stride, int64_t pstride, double noise_var,
+                                     uint64_t seed, void* stream) {
+  const int64_t W = gm_panel_width(K);
+  if (!c || !X || P < 0 || K < 0 || d < 0 || noise_var < 0 || (K > 0 && W == 0) ||
+      panel_stride < K * W || (P > 1 && pstride < (d + W - 1) / W * panel_stride))
+    return fail(GM_ERR_INVALID, "gm_oma_philox_batched_panels_f32: bad args");
+  if (P == 0 || K == 0 || d == 0) return GM_OK;
+  if (c->d_total > 0)
+    return fail(GM_ERR_UNSUPPORTED, "gm_oma_philox_batched_panels_f32: not on a d-sharded context");
+  HIPCHK(hipSetDevice(c->device));
+  int wshift = 0;
+  while ((int64_t)1 << wshift < W) ++wshift;
+  HIPCHK(launch_oma_philox(X, K, d, panel_stride, d, 0, (float)std::sqrt(noise_var), seed,
+                           reinterpret_cast<hipStream_t>(stream), wshift, P, P > 1 ? pstride : 0));
   return GM_OK;
 }
 

@@ -102,7 +102,7 @@ typedef struct gm_opts {
     gm_noise_cb noise_cb;     /* GM_NOISE_HOST */
     void* noise_user;
     int32_t check_every;      /* host convergence poll interval in iterations; 0 = auto */
-    int32_t layout;           /* gm_layout of X (gm_weiszfeld_f32 only; batched: ROWS) */
+    int32_t layout;           /* gm_layout of X (gm_weiszfeld_f32 and gm_weiszfeld_batched_f32) */
 } gm_opts;
 
 enum gm_guard {
@@ -163,7 +163,9 @@ int64_t gm_panel_width(int64_t K);
  * covers all P problems; each stops at its own tol test (gm2) or runs maxiter
  * (gm).  Options are shared; GM_MODE_AIRCOMP uses Philox only, problem p keyed
  * with seed + p * 0x9E3779B97F4A7C15.  results: P entries or NULL.  Not
- * combinable with d-sharding. */
+ * combinable with d-sharding.  opts->layout = GM_LAYOUT_PANELS: problem p at X + p*ldp
+ * is in the panel layout [ceil(d/W)][K][W] (W = gm_panel_width(K)) with panel stride
+ * ldx >= K*W, ldp >= ceil(d/W)*ldx; the same results as the row-major call. */
 int gm_weiszfeld_batched_f32(gm_ctx* ctx, const float* X, int64_t P, int64_t K, int64_t d,
                              int64_t ldx, int64_t ldp, const float* guess0, int64_t ldg,
                              float* out, int64_t ldo, const gm_opts* opts, gm_result* results,
@@ -202,6 +204,13 @@ int gm_oma_philox_f32(gm_ctx* ctx, float* X, int64_t K, int64_t d, int64_t ldx,
  * problem p's draws are gm_oma_philox_f32's with seed + p * 0x9E3779B97F4A7C15. */
 int gm_oma_philox_batched_f32(gm_ctx* ctx, float* X, int64_t P, int64_t K, int64_t d, int64_t ldx,
                               int64_t pstride, double noise_var, uint64_t seed, void* stream);
+
+/* Batched OMA on P problems in the panel layout: problem p at X + p*pstride is
+ * [ceil(d/W)][K][W] with panel_stride >= K*W; the same draws as
+ * gm_oma_philox_batched_f32 on the row-major problems. */
+int gm_oma_philox_batched_panels_f32(gm_ctx* ctx, float* X, int64_t P, int64_t K, int64_t d,
+                                     int64_t panel_stride, int64_t pstride, double noise_var,
+                                     uint64_t seed, void* stream);
 
 /* The same OMA on client updates in the panel layout (GM_LAYOUT_PANELS: X as
  * [ceil(d/W)][K][W], W = gm_panel_width(K), panel_stride >= K*W): identical draws

@@ -47,9 +47,9 @@ def test_panels_bit_identical_to_rows(K, d, agg):
     b = f(P, dict(opts))
     rb = bz().aggregators.last_result
     assert rb.algo == "stream"
-    if d % 4 == 0 and not 128 < K <= 256:
-        # the row-major call runs the same float4 tile: same chunks, same order
-        # (at 128 < K <= 256 its INIT pass takes a wider tile, api.hip light_cfg)
+    if d % 4 == 0 and not (32 < K <= 64 or 128 < K <= 256):
+        # the row-major call runs the same float4 tile: same chunks, same order (at
+        # 32 < K <= 64 and 128 < K <= 256 panels have a tile of their own, api.hip pick_cfg)
         assert torch.equal(a, b)
         assert (ra.iters, ra.converged) == (rb.iters, rb.converged)
         assert ra.last_movement == rb.last_movement or (np.isnan(ra.last_movement)
@@ -77,7 +77,7 @@ def test_panels_match_reference_gm2(name):
 
 
 def test_panels_store_rows_and_default_guess():
-    K, d = 40, 1236                           # d % 4 == 0: the same float4 tile
+    K, d = 24, 1236                           # d % 4 == 0, K <= 32: the same float4 tile
     X, _ = _data(K, d, seed=5)
     P = bz().ClientPanels(K, d)
     for k in range(K):
