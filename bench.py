@@ -76,6 +76,9 @@ def parse():
                         "is timed too (alt_layout in the JSON line).")
     p.add_argument("--alt-steps", type=int, default=None,
                    help="steps for the other layout's measurement (0 = skip)")
+    p.add_argument("--separate-oma", action="store_true",
+                   help="c5 prenoise reading: OMA as its own pass instead of fused into gm2's "
+                        "first pass (A/B)")
     p.add_argument("--soak", type=float, default=8.0,
                    help="seconds of untimed aggregations after the timed region (0 = none): the "
                         "GPU stays busy long enough for an outside utilisation sampler to see it")
@@ -262,9 +265,12 @@ def run_c5(args, json_out):
             t0 = time.perf_counter()
             if var == 0.0:
                 _, res = gm2_batched(X, opts)
-            elif reading == "prenoise":
+            elif reading == "prenoise" and args.separate_oma:
                 oma_batched(X, var, seed=31 + vi * 1000 + c0)
                 _, res = gm2_batched(X, opts)
+            elif reading == "prenoise":
+                # the pre-noise fused into gm2's first pass (same draws as oma_batched)
+                _, res = gm2_batched(X, dict(opts, pre_oma_var=var, pre_oma_seed=31 + vi * 1000 + c0))
             else:
                 _, res = gm_batched(X, dict(opts, noise_var=var, seed=31 + vi * 1000 + c0))
             torch.cuda.synchronize(dev)
@@ -322,7 +328,10 @@ def run_c5(args, json_out):
                 "guess N(0,0.01^2))",
         "config": {"workload": f"c5: {n_prob} independent gm2 problems K={K} x d={d} fp32 over "
                                f"var {list(C5_VARS)} x B {list(C5_BYZ)}, reading '{args.reading}'"
-                               + (" (OMA pre-noise then gm2, M:351-353)"
+                               + ((" (OMA pre-noise then gm2, M:351-353; separate OMA pass)"
+                                   if args.separate_oma else
+                                   " (OMA pre-noise then gm2, M:351-353; the pre-noise fused "
+                                   "into gm2's first pass)")
                                   if args.reading == "prenoise" else " (AirComp gm for var > 0)"),
                    "K": K, "d": d, "problems": n_prob, "mean_iters": mean_it,
                    "parallelism": "batched (one launch per pass covers every problem of a group)",

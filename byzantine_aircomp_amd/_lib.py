@@ -12,7 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMAGG_LIB", os.path.join(HERE, "libgmagg.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 GM_MODE_IDEAL, GM_MODE_AIRCOMP = 0, 1
 GM_NOISE_PHILOX, GM_NOISE_HOST = 0, 1
@@ -42,6 +42,9 @@ class GmOpts(C.Structure):
         ("noise_user", C.c_void_p),
         ("check_every", C.c_int32),
         ("layout", C.c_int32),
+        ("pre_oma", C.c_int32),
+        ("pre_oma_var", C.c_double),
+        ("pre_oma_seed", C.c_uint64),
     ]
 
 

@@ -209,11 +209,22 @@ def _weiszfeld(wList: torch.Tensor, options: dict, aircomp: bool):
     if aircomp:
         opts.update({"noise_var": None, "P_max": 1})
     opts.update(options or {})
+    # pre_oma_var: the reference's OMA(weight_f, var) before a non-gm aggregator
+    # (M:351-352), in place on wList, fused into the first streaming pass (pre_oma_seed
+    # keys the Philox draws as OMA(..., seed=)).  With the default guess (the column mean
+    # of the NOISY rows) it runs as the separate OMA first.
+    pre_var = None if aircomp else opts.get("pre_oma_var")
+    pre_seed = _seed({"seed": opts.get("pre_oma_seed")}) if pre_var is not None else 0
+    if pre_var is not None and (opts.get("guess") is None or wList.device.type != "cuda"):
+        OMA(wList, float(pre_var), seed=pre_seed)
+        pre_var = None
     guess = opts.get("guess")
     if guess is None:
         guess = wList.mean(dim=0)
     maxiter = int(opts["maxiter"])
     if maxiter <= 0:                        # M:145 / M:173 loop body never runs
+        if pre_var is not None:
+            OMA(wList, float(pre_var), seed=pre_seed)
         last_result = GMResult(0, float("nan"), False, "none")
         return guess
     layout = _lib.GM_LAYOUT_ROWS
@@ -240,6 +251,10 @@ def _weiszfeld(wList: torch.Tensor, options: dict, aircomp: bool):
     o.algo = _ALGOS[opts.get("algo", "auto")]
     o.check_every = int(opts.get("check_every", 0))
     o.layout = layout
+    if pre_var is not None:
+        o.pre_oma = 1
+        o.pre_oma_var = float(pre_var)
+        o.pre_oma_seed = pre_seed
     cb = None
     if aircomp:
         var = opts["noise_var"]

@@ -97,6 +97,14 @@ def _run(X, options: dict, aircomp: bool):
         buf, ldx, ldp = X, X.stride(1), X.stride(0)
     opts = {"maxiter": 200, "tol": 1e-5, "noise_var": None, "P_max": 1}
     opts.update(options or {})
+    # pre_oma_var (gm2): the `--agg gm2 --var v` pre-noise (M:351-352) in place, fused
+    # into the INIT pass; problem p keyed pre_oma_seed + p * SEED_STRIDE as oma_batched.
+    # The default guess is the mean of the NOISY rows: then the separate OMA runs first.
+    pre_var = None if aircomp else opts.get("pre_oma_var")
+    pre_seed = int(opts.get("pre_oma_seed", 2021)) & 0xFFFFFFFFFFFFFFFF
+    if pre_var is not None and opts.get("guess") is None:
+        oma_batched(X, float(pre_var), seed=pre_seed)
+        pre_var = None
     guess = opts.get("guess")
     if guess is None:
         guess = (X.to_rows() if panels else X).mean(dim=1)
@@ -111,6 +119,10 @@ def _run(X, options: dict, aircomp: bool):
     o.mode = _lib.GM_MODE_AIRCOMP if aircomp else _lib.GM_MODE_IDEAL
     o.check_every = int(opts.get("check_every", 0))
     o.layout = _lib.GM_LAYOUT_PANELS if panels else _lib.GM_LAYOUT_ROWS
+    if pre_var is not None:
+        o.pre_oma = 1
+        o.pre_oma_var = float(pre_var)
+        o.pre_oma_seed = pre_seed
     if aircomp:
         var = opts["noise_var"]
         o.has_noise = int(var is not None)

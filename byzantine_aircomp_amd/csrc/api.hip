@@ -563,7 +563,29 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   const int64_t d_total = sharded ? c->d_total : d;
   const int64_t col_off = sharded ? c->d_offset : 0;
   gm_result r{};
+  // pre_oma: the reference's OMA(weight_f, var) before a non-gm aggregator (M:351-352),
+  // applied to X in place.  The streaming path fuses it into its INIT pass (MODE 4: one
+  // read + write of X instead of OMA's read + write and INIT's read); every other path
+  // runs the standalone kernel first.  Draws as gm_oma_philox_f32 / _panels_f32.
+  if (o->pre_oma && (o->mode != GM_MODE_IDEAL || !(o->pre_oma_var >= 0)))
+    return fail(GM_ERR_INVALID, "pre_oma: gm2 only (the reference applies OMA before non-gm "
+                "aggregators, M:351), noise variance >= 0");
+  bool oma_pending = o->pre_oma != 0;
+  auto apply_oma = [&]() -> int {
+    if (!oma_pending) return GM_OK;
+    oma_pending = false;
+    int wshift = 0;
+    if (o->layout == GM_LAYOUT_PANELS) {
+      const int64_t W = gm_panel_width(K);
+      while ((int64_t)1 << wshift < W) ++wshift;
+    }
+    HIPCHK(launch_oma_philox(const_cast<float*>(X), K, d, ldx, d_total, col_off,
+                             (float)std::sqrt(o->pre_oma_var), o->pre_oma_seed, s, wshift));
+    return GM_OK;
+  };
   if (o->maxiter == 0) {
+    int rco = apply_oma();
+    if (rco) return rco;
     HIPCHK(hipMemcpyAsync(out, guess0, sizeof(float) * d, hipMemcpyDeviceToDevice, s));
     r.last_movement = NAN;
     if (res) *res = r;
@@ -595,6 +617,8 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
         (algo == GM_ALGO_GRAM && gram_ok)) {
       static const bool unguarded = getenv("GMAGG_GRAM_UNGUARDED") != nullptr;
       bool rejected = false;
+      int rco = apply_oma();
+      if (rco) return rco;
       const int rc0 = run_gram(c, X, K, d, W, guess0, out, o, res, cfg, s, true,
                                algo == GM_ALGO_AUTO || !unguarded, &rejected, ldx);
       if (rc0 || !rejected) return rc0;
@@ -628,6 +652,8 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
                   "other rank's (use sharded.shard_range + contiguous shards)",
                   (long long)d_total);
     bool rejected = false;
+    int rco = apply_oma();
+    if (rco) return rco;
     const int rc0 = run_gram(c, X, K, d, ldx, guess0, out, o, res, cfg, s, true, true, &rejected);
     if (rc0 || !rejected) return rc0;
     guard_rejected = true;
@@ -642,6 +668,8 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
     int cpb = 0, nbr = 0;
     if (resident_plan(cfg, nch, c->num_cu, &cpb, &nbr)) {
       bool timed_out = false;
+      int rco = apply_oma();
+      if (rco) return rco;
       const int rc0 = run_resident(c, X, K, d, ldx, guess0, out, o, res, cfg, cpb, nbr, s,
                                    &timed_out);
       if (rc0 || !timed_out) return rc0;
@@ -675,6 +703,8 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
     // the bare Gram path, whose closing pass is the lighter sum-only tile.)
     static const bool unguarded = getenv("GMAGG_GRAM_UNGUARDED") != nullptr;
     bool rejected = false;
+    int rco = apply_oma();
+    if (rco) return rco;
     const int rc0 = run_gram(c, X, K, d, ldx, guess0, out, o, res, cfg, s, split, !unguarded,
                              &rejected);
     if (rc0 || !rejected) return rc0;
@@ -767,10 +797,24 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       a.slab = w.slab; a.slab_stride = S;
       a.noise = noise_kind; a.hnoise = w.hnoise; a.seed = o->seed; a.iter = t; a.col_off = col_off;
       a.panel_stride = panels ? ldx : 0;
-      HIPCHK(launch_pass(init ? cfg_i : cfg, init ? init_mode : 0, init ? nb_init : nb_step, a, s));
+      int mode = init ? init_mode : 0;
+      if (init && oma_pending) {
+        // the fused OMA needs float4 groups = Philox blocks: V = 4, 4-aligned shards
+        if (cfg_i.V == 4 && col_off % 4 == 0 && init_mode == 1) {
+          mode = 4;
+          a.oma_sd = (float)std::sqrt(o->pre_oma_var);
+          a.oma_seed = o->pre_oma_seed;
+          oma_pending = false;
+        } else {
+          int rco = apply_oma();
+          if (rco) return rco;
+        }
+      }
+      HIPCHK(launch_pass(init ? cfg_i : cfg, mode, init ? nb_init : nb_step, a, s));
       if (!init) { rc2 = record_pass_end(c, s, e0, e1); if (rc2) return rc2; }
       HIPCHK(launch_slab_reduce(w.slab, init ? nb_init : nb_step, S, w.sums, w.st, s));
     } else {
+      if (init) { int rco = apply_oma(); if (rco) return rco; }
       HIPCHK(launch_twopass(init, X, K, d, ldx, g_old, g_new, w.coef, w.st, noise_kind, w.hnoise,
                             o->seed, t, col_off, w.slab, nb, w.sums, s));
       if (!init) { rc2 = record_pass_end(c, s, e0, e1); if (rc2) return rc2; }
@@ -892,11 +936,28 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
   if (o->mode == GM_MODE_AIRCOMP && o->noise_source != GM_NOISE_PHILOX)
     return fail(GM_ERR_UNSUPPORTED, "batched AirComp uses Philox noise only");
   if (c->d_total > 0) return fail(GM_ERR_UNSUPPORTED, "batched problems are not d-sharded");
+  if (o->pre_oma && (o->mode != GM_MODE_IDEAL || !(o->pre_oma_var >= 0)))
+    return fail(GM_ERR_INVALID, "pre_oma: gm2 only, noise variance >= 0");
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   WsOrder order(c, s);
   HIPCHK(order.err);
+  // pre_oma (the reference's `--agg gm2 --var v` pre-noise, M:351-352): fused into the
+  // INIT pass when the tile takes float4 groups, else the standalone batched OMA first;
+  // problem p keyed pre_oma_seed + p * kSeedStride either way
+  const float oma_sd = (float)std::sqrt(std::max(0.0, o->pre_oma_var));
+  auto oma_standalone = [&]() -> int {
+    int wshift = 0;
+    while (panels && ((int64_t)1 << wshift) < Wp) ++wshift;
+    HIPCHK(launch_oma_philox(const_cast<float*>(X), K, d, ldx, d, 0, oma_sd, o->pre_oma_seed, s,
+                             wshift, P, P > 1 ? ldp : 0));
+    return GM_OK;
+  };
   if (o->maxiter == 0) {
+    if (o->pre_oma) {
+      const int rco = oma_standalone();
+      if (rco) return rco;
+    }
     HIPCHK(hipMemcpy2DAsync(out, ldo * 4, guess0, ldg * 4, d * 4, P, hipMemcpyDeviceToDevice, s));
     if (results)
       for (int64_t p = 0; p < P; ++p) results[p] = gm_result{0, NAN, 0, GM_ALGO_STREAM, GM_GUARD_NONE, 0};
@@ -977,10 +1038,21 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
     a.coef = coef; a.st = st; a.slab = slab; a.slab_stride = init ? S : K + 2;
     a.noise = noise_kind; a.seed = o->seed; a.iter = t;
     a.panel_stride = panels ? ldx : 0;
+    int mode = init ? init_mode : 0;
+    if (init && o->pre_oma) {
+      if (cfg.V == 4 && init_mode == 1) {
+        mode = 4;
+        a.oma_sd = oma_sd;
+        a.oma_seed = o->pre_oma_seed;
+      } else {
+        const int rco = oma_standalone();
+        if (rco) return rco;
+      }
+    }
     hipEvent_t e0, e1;
     int rc2 = init ? GM_OK : record_pass_begin(c, s, &e0, &e1);
     if (rc2) return rc2;
-    HIPCHK(launch_pass(cfg, init ? init_mode : 0, nbp, a, s, (int)P));
+    HIPCHK(launch_pass(cfg, mode, nbp, a, s, (int)P));
     if (!init) { rc2 = record_pass_end(c, s, e0, e1); if (rc2) return rc2; }
     HIPCHK(launch_slab_reduce(slab, nbp, init ? S : K + 2, sums, st, s, (int)P, S));
     return GM_OK;

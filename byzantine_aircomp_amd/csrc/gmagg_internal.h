@@ -55,6 +55,11 @@ struct PassArgs {
   // > 0: X is in the panel layout [ceil(d/J)][K][J] with this many elements
   // between panels (J = the tile's chunk width); 0: row-major [K][ldx].
   int64_t panel_stride;
+  // MODE 4 (INIT + OMA): the reference's OMA pre-noise (M:351-352, M:385-394) applied to
+  // the tile in registers and written back before the INIT distances; Philox keyed by
+  // oma_seed (+ p * kSeedStride for batched problem p), draws as gm_oma_philox_f32's
+  float oma_sd;
+  uint64_t oma_seed;
 };
 
 constexpr uint64_t kSeedStride = 0x9E3779B97F4A7C15ull;
@@ -79,7 +84,8 @@ struct KspaceArgs {
   int* n_done;            // problems whose tol test has fired (nullable)
 };
 
-// Streaming pass (stream_pass.hip).  mode: 0 step, 1 init, 2 init + ||x_k||^2.
+// Streaming pass (stream_pass.hip).  mode: 0 step, 1 init, 2 init + ||x_k||^2, 3 Gram
+// closing sum, 4 init after OMA pre-noise written back to X (V = 4 tiles).
 hipError_t launch_pass(const PassCfg& cfg, int mode, int grid, const PassArgs& a, hipStream_t s,
                        int problems = 1);
 int pass_blocks_per_cu(const PassCfg& cfg, int mode);

@@ -68,10 +68,7 @@ __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t
   for (int64_t r = blockIdx.y; r < K; r += gridDim.y) {
     const int64_t pi = r / Kp, k = r - pi * Kp;
     const uint64_t seed = seed0 + (uint64_t)pi * kSeedStride;
-    float h[4];
-    normal4_hw(seed, kStreamOmaChannel, 0, (uint64_t)k, h);
-    const float a = h[0] * 0.70710678118654752f, b = h[1] * 0.70710678118654752f;
-    const float scale = sd / sqrtf(a * a + b * b);
+    const float scale = oma_row_scale(seed, (uint64_t)k, sd);
     float* row = (wshift ? X + (k << wshift) : X + k * ldx) + pi * pstride;
     // Step s covers groups g0 + q*T (q < U).  Step s+1's loads are issued before
     // step s's Philox math and stores, so each thread keeps U loads in flight
@@ -108,24 +105,24 @@ __global__ void __launch_bounds__(256) oma_philox(float* __restrict__ X, int64_t
         const uint64_t c0 = (uint64_t)(col_off + j0);
         float z[8];
         normal4_hw(seed, kStreamOmaNoise, (uint64_t)k, c0 >> 2, z);
-        float add[4];
+        float zz[4];
         if constexpr (ALIGNED) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u) add[u] = scale * z[u];
+          for (int u = 0; u < 4; ++u) zz[u] = z[u];
         } else {
           const int sh = (int)(c0 & 3);
           normal4_hw(seed, kStreamOmaNoise, (uint64_t)k, (c0 >> 2) + 1, z + 4);
 #pragma unroll
-          for (int u = 0; u < 4; ++u) add[u] = scale * z[u + sh];
+          for (int u = 0; u < 4; ++u) zz[u] = z[u + sh];
         }
         if (full[q]) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u) v[q][u] = v[q][u] + add[u];
+          for (int u = 0; u < 4; ++u) v[q][u] = oma_noisy(v[q][u], scale, zz[u]);
           __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(rp[q] + j0));
         } else {
 #pragma unroll
           for (int u = 0; u < 4; ++u)
-            if (j0 + u < d) rp[q][j0 + u] = rp[q][j0 + u] + add[u];
+            if (j0 + u < d) rp[q][j0 + u] = oma_noisy(rp[q][j0 + u], scale, zz[u]);
         }
       }
 #pragma unroll

@@ -99,6 +99,22 @@ __device__ __forceinline__ void normal4_hw(uint64_t seed, uint32_t stream, uint6
   box_muller_hw(r.z, r.w, &out[2], &out[3]);
 }
 
+// OMA (M:385-394) with Philox draws: client k's equalisation scale sd / |h_k|, h_k ~ CN(0, 1)
+// from the block keyed (row k), and the noisy element x + scale * z.  Contraction off:
+// the standalone OMA kernel and the OMA fused into a streaming pass run these same two
+// functions, so their results are identical bit for bit.
+__device__ __forceinline__ float oma_row_scale(uint64_t seed, uint64_t k, float sd) {
+#pragma clang fp contract(off)
+  float h[4];
+  normal4_hw(seed, kStreamOmaChannel, 0, k, h);
+  const float a = h[0] * 0.70710678118654752f, b = h[1] * 0.70710678118654752f;
+  return sd / sqrtf(a * a + b * b);
+}
+__device__ __forceinline__ float oma_noisy(float x, float scale, float z) {
+#pragma clang fp contract(off)
+  return x + scale * z;
+}
+
 // One standard normal for element `idx` (uses half of a Philox block): the AirComp
 // column noise, drawn by the pass's finisher threads between two block barriers, on
 // the hardware Box-Muller.  Device-only: every call site that regenerates a draw

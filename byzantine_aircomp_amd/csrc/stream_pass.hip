@@ -33,7 +33,9 @@ struct Tile {
   float hn;      // STEP finisher thread, host noise: its column's draw
 };
 
-// MODE: 0 step, 1 init, 2 init + ||x_k||^2, 3 Gram closing sum.  SCHED 0: load a
+// MODE: 0 step, 1 init, 2 init + ||x_k||^2, 3 Gram closing sum, 4 init after the OMA
+// pre-noise (the tile gets the reference's per-client AWGN, M:385-394, in registers and is
+// written back: one read + one write of X instead of OMA's read + write and INIT's read).  SCHED 0: load a
 // chunk, then reduce it; 1 (PIPE): chunk c+1's loads are in flight while chunk
 // c is reduced (two tiles of registers); 2 (ROLL): row i of chunk c+1 is loaded
 // into the registers phase B has just freed (one tile).
@@ -46,8 +48,10 @@ template <int V, int NW, int LPR, int R, int MODE, int SCHED, int OCC = 1, bool 
 __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs a) {
   constexpr bool PIPE = SCHED == 1, ROLL = SCHED == 2;
   constexpr bool SUM_ONLY = MODE == 3;     // closing pass of the Gram variant: g = sum c_k x_k
-  constexpr bool INIT = MODE == 1 || MODE == 2;
+  constexpr bool OMA_INIT = MODE == 4;
+  constexpr bool INIT = MODE == 1 || MODE == 2 || OMA_INIT;
   constexpr bool WANT_R = MODE == 2;
+  static_assert(!OMA_INIT || V == 4, "fused OMA: one Philox block per float4 group");
   constexpr int QW = 64 / LPR;
   constexpr int NRG = NW * QW;
   constexpr int J = LPR * V;
@@ -69,6 +73,7 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
     a.st += pb;
     a.slab += pb * (int64_t)gridDim.x * a.slab_stride;
     a.seed += (uint64_t)pb * kSeedStride;
+    a.oma_seed += (uint64_t)pb * kSeedStride;
   }
   if (!SUM_ONLY && a.st->done) return;
 
@@ -93,6 +98,14 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
   const uint32_t goff = (uint32_t)q * (uint32_t)a.ldx;
   const uint32_t poff = ((uint32_t)q * J + (uint32_t)(c * V)) * 4u;   // PANEL: bytes from the wave's rows
 
+  // fused OMA: this thread's rows' equalisation scales sd / |h_k| (row k keyed as in
+  // the standalone OMA kernel)
+  float osc[OMA_INIT ? R : 1];
+  if constexpr (OMA_INIT) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      osc[i] = rval[i] ? oma_row_scale(a.oma_seed, (uint64_t)(rg + NRG * i), a.oma_sd) : 0.f;
+  }
   float wt[OCC > 1 ? 1 : R];
   float a_noise = 0.f;
   if constexpr (!INIT) {
@@ -158,8 +171,38 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
   // consumed row i of chunk ch, so the next chunk's loads are in flight during
   // phase B, the row reductions and the next chunk's barriers (no second tile).
   int par = 0;   // INIT: chunk parity -> s_g buffer
+  // fused OMA: noise the tile's real elements (element (k, global column c) takes normal
+  // c & 3 of the Philox block (row k, c >> 2): V = 4 columns = one block) and write them
+  // back where they were read; padding columns and rows are left untouched
+  auto oma_tile = [&](int64_t ch, T& t) {
+    const int64_t col = ch * J + (int64_t)c * V;
+    if (ch >= nch || col >= d) return;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (!rval[i]) continue;
+      const int64_t k = rg + (int64_t)NRG * i;
+      float z[4];
+      normal4_hw(a.oma_seed, kStreamOmaNoise, (uint64_t)k, (uint64_t)(a.col_off + col) >> 2, z);
+#pragma unroll
+      for (int v = 0; v < V; ++v) t.x[i][v] = oma_noisy(t.x[i][v], osc[i], z[v]);
+      float* dst;
+      if constexpr (PANEL)
+        dst = const_cast<float*>(a.X) + ch * a.panel_stride + k * J + c * V;
+      else
+        dst = const_cast<float*>(base[i]) + goff + col;
+      if (col + V <= d) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<f4*>(dst) = f4{t.x[i][0], t.x[i][1], t.x[i][2], t.x[i][3]};
+      } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+          if (col + v < d) dst[v] = t.x[i][v];
+      }
+    }
+  };
   auto process = [&](int64_t ch, T& t, int64_t nxt) {
     float gv[V];
+    if constexpr (OMA_INIT) oma_tile(ch, t);
     if constexpr (INIT) {
       // the guess at this chunk's columns -> LDS (buffer by parity: a thread still
       // reading the previous chunk's buffer has not passed this chunk's barrier)
@@ -362,6 +405,9 @@ static const void* pass_fn_mode(int mode, bool panel) {
     case 0: return pass_fn<V, NW, LPR, R, 0, OCC>(panel);
     case 1: return pass_fn<V, NW, LPR, R, 1, OCC>(panel);
     case 2: return pass_fn<V, NW, LPR, R, 2, OCC>(panel);
+    case 4:
+      if constexpr (V == 4) return pass_fn<V, NW, LPR, R, 4, OCC>(panel);
+      else return nullptr;
     default: return pass_fn<V, NW, LPR, R, 3, OCC>(panel);
   }
 }

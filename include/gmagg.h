@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GMAGG_ABI_VERSION 2
+#define GMAGG_ABI_VERSION 3
 
 enum gm_status {
     GM_OK = 0,
@@ -103,6 +103,13 @@ typedef struct gm_opts {
     void* noise_user;
     int32_t check_every;      /* host convergence poll interval in iterations; 0 = auto */
     int32_t layout;           /* gm_layout of X (gm_weiszfeld_f32 and gm_weiszfeld_batched_f32) */
+    /* pre_oma = 1 (gm2 only): first apply OMA(X, pre_oma_var) IN PLACE, as the reference
+     * does before every non-gm aggregator when --var is set (MNIST_Air_weight.py:351-352),
+     * with the draws of gm_oma_philox_f32 (batched: problem p keyed pre_oma_seed + p *
+     * 0x9E3779B97F4A7C15).  The streaming path fuses it into its first pass. */
+    int32_t pre_oma;
+    double pre_oma_var;
+    uint64_t pre_oma_seed;
 } gm_opts;
 
 enum gm_guard {

@@ -429,3 +429,63 @@ def test_gram_f16_range_overflow_falls_back(spike):
     assert res.algo == "gram" and res.gram_kind == "bf16_split"
     assert rel_l2(got.cpu().numpy(), want.numpy()) <= TOL
     assert abs(res.iters - tr.iters) <= ITER_SLACK
+
+
+@pytest.mark.parametrize("K,d,layout,algo", [
+    (1000, 4096, "rows", "stream"),       # fused into the INIT pass (float4 rows)
+    (1000, 4100, "panels", "auto"),       # fused, panels (partial last float4 group of panels)
+    (300, 2051, "rows", "stream"),        # float1 rows: the standalone OMA first
+    (50, 7850, "rows", "auto"),           # register-resident path: standalone OMA first
+    (256, 1 << 18, "rows", "auto"),       # guarded Gram: standalone OMA first
+    (200, (1 << 18) + 64, "panels", "auto"),
+])
+def test_pre_oma_equals_oma_then_gm2(K, d, layout, algo):
+    """gm2 with pre_oma_var (the reference's OMA(weight_f, var) before the aggregator,
+    M:351-352) == OMA then gm2: the same noisy X, bit for bit, and the same aggregate."""
+    import byzantine_aircomp_amd as bz
+    g = torch.Generator().manual_seed(K + d)
+    X = 0.05 * torch.randn(K, d, generator=g)
+    X[K - K // 5:] += 0.25
+    g0 = (0.01 * torch.randn(d, generator=g)).cuda()
+    X = X.cuda()
+
+    def fresh():
+        return bz.ClientPanels.from_rows(X) if layout == "panels" else X.clone()
+
+    opts = {"maxiter": 30, "tol": 1e-5, "guess": g0, "algo": algo}
+    A = fresh()
+    bz.OMA(A, 1e-2, seed=77)
+    a = bz.gm2(A, dict(opts))
+    ra = bz.aggregators.last_result
+    B = fresh()
+    b = bz.gm2(B, dict(opts, pre_oma_var=1e-2, pre_oma_seed=77))
+    rb = bz.aggregators.last_result
+    da = A.data if layout == "panels" else A
+    db = B.data if layout == "panels" else B
+    assert torch.equal(da, db)
+    assert torch.equal(a, b)
+    assert (ra.iters, ra.algo) == (rb.iters, rb.algo)
+
+
+@pytest.mark.parametrize("layout", ["rows", "panels"])
+def test_batched_pre_oma_equals_oma_then_gm2(layout):
+    from byzantine_aircomp_amd.batched import ProblemPanels, gm2_batched, oma_batched
+    P, K, d = 6, 50, 10000
+    g = torch.Generator().manual_seed(3)
+    X = (0.05 * torch.randn(P, K, d, generator=g)).cuda()
+    g0 = (0.01 * torch.randn(P, d, generator=g)).cuda()
+
+    def fresh():
+        return ProblemPanels.from_rows(X) if layout == "panels" else X.clone()
+
+    opts = {"maxiter": 30, "tol": 1e-5, "guess": g0}
+    A = fresh()
+    oma_batched(A, 1e-2, seed=123)
+    a, ra = gm2_batched(A, dict(opts))
+    B = fresh()
+    b, rb = gm2_batched(B, dict(opts, pre_oma_var=1e-2, pre_oma_seed=123))
+    da = A.data if layout == "panels" else A
+    db = B.data if layout == "panels" else B
+    assert torch.equal(da, db)
+    assert torch.equal(a, b)
+    assert [r.iters for r in ra] == [r.iters for r in rb]
