@@ -215,8 +215,10 @@ def _weiszfeld(wList: torch.Tensor, options: dict, aircomp: bool):
     # of the NOISY rows) it runs as the separate OMA first.
     pre_var = None if aircomp else opts.get("pre_oma_var")
     pre_seed = _seed({"seed": opts.get("pre_oma_seed")}) if pre_var is not None else 0
-    if pre_var is not None and (opts.get("guess") is None or wList.device.type != "cuda"):
-        OMA(wList, float(pre_var), seed=pre_seed)
+    if pre_var is not None and (opts.get("guess") is None or wList.device.type != "cuda"
+                                or _noise_source(opts) == _lib.GM_NOISE_HOST):
+        # (the reference's own draws are host-side: OMA replays them itself)
+        OMA(wList, float(pre_var), noise_source=opts.get("noise_source"), seed=pre_seed)
         pre_var = None
     guess = opts.get("guess")
     if guess is None:

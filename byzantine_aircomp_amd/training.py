@@ -221,7 +221,11 @@ def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # 
     params = clients.params
     is_gm = aggregate.__name__ == "gm"
     if noise_var is not None and not is_gm:
+        from . import aggregators as _agg
         from .aggregators import OMA
+        # our gm2 takes the pre-noise inside its first streaming pass (options
+        # pre_oma_var: the same draws, seed drawn from torch's generator as OMA's is)
+        fuse_oma = aggregate is _agg.gm2 and _agg._noise_source({}) == _agg._lib.GM_NOISE_PHILOX
     for r in range(rounds):
         for _ in range(displayInterval):
             for node in range(K):
@@ -244,7 +248,10 @@ def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # 
             options = {"maxiter": 1000, "tol": 1e-5, "eta": 1, "noise_var": noise_var,
                        "guess": clients.flat(), "honestSize": honestSize}     # M:349-350
             if noise_var is not None and not is_gm:
-                OMA(X, noise_var)                         # M:351-352
+                if fuse_oma:
+                    options["pre_oma_var"] = noise_var    # M:351-352, fused into gm2
+                else:
+                    OMA(X, noise_var)                     # M:351-352
             clients.load(aggregate(X, options))           # M:353-358
         paths["var"].append(getVarience(clients.X, honestSize).cpu())
         tl, ta = train_eval()
