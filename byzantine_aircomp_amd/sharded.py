@@ -136,6 +136,15 @@ class ShardedGM:
         o.mode = _lib.GM_MODE_AIRCOMP if aircomp else _lib.GM_MODE_IDEAL
         o.algo = _ALGOS[opts.get("algo", "auto")]
         o.layout = layout
+        if not aircomp and opts.get("pre_oma_var") is not None:
+            # OMA pre-noise on this rank's columns (keyed by global column: the shards
+            # together draw what one unsharded OMA would), fused into the first pass
+            if opts.get("pre_oma_seed") is None:
+                raise ValueError("sharded pre-noise needs options['pre_oma_seed'] identical on "
+                                 "every rank")
+            o.pre_oma = 1
+            o.pre_oma_var = float(opts["pre_oma_var"])
+            o.pre_oma_seed = _seed({"seed": opts["pre_oma_seed"]})
         if aircomp:
             var = opts["noise_var"]
             o.has_noise = int(var is not None)

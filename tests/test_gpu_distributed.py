@@ -149,3 +149,26 @@ def test_sharded_requires_guess_and_seed(world1):
             sg.gm2(torch.zeros(8, 1000, device="cuda"), {"guess": torch.ones(1000, device="cuda")})
     finally:
         sg.close()
+
+
+@pytest.mark.parametrize("layout", ["rows", "panels"])
+def test_sharded_pre_oma_world1(world1, layout):
+    """ShardedGM gm2 with the fused OMA pre-noise == OMA then the unsharded gm2."""
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd.sharded import ShardedGM
+    K, d = 1000, 100_000
+    X, g0 = _fill(K, d, 200)
+    opts = {"maxiter": 1000, "tol": 1e-5, "guess": g0}
+    A = X.clone()
+    bz.OMA(A, 1e-2, seed=41)
+    want = bz.gm2(A, dict(opts))
+    sg = ShardedGM(d, transport="torch")
+    try:
+        B = bz.ClientPanels.from_rows(X) if layout == "panels" else X.clone()
+        got = sg.gm2(B, dict(opts, pre_oma_var=1e-2, pre_oma_seed=41))
+        torch.cuda.synchronize()
+    finally:
+        sg.close()
+    Bn = B.to_rows() if layout == "panels" else B
+    assert torch.equal(Bn, A)
+    assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-6
