@@ -1,0 +1,88 @@
+"""End-to-end federated training steps (the build's own loop,
+training.SGD, M:226-372) on the GPU: K = 50 clients (45 honest + 5 classflip), the
+reference's MNIST MLP (d = 7,850), synthetic MNIST-shaped data (no dataset here).  One
+step = 50 sequential client SGD steps + the aggregation; the aggregation's own share is
+timed by wrapping the aggregator (device-synchronised).
+
+    python tools/loop_bench.py [--steps 20] [--out profiles/rNN_loop.jsonl]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def synthetic_mnist(seed, n):
+    proto = np.random.default_rng(600).standard_normal((10, 1, 28, 28)).astype(np.float32)
+    r = np.random.default_rng(seed)
+    y = r.integers(0, 10, n).astype(np.int64)
+    x = (proto[y] + 2.0 * r.standard_normal((n, 1, 28, 28))).astype(np.float32)
+    return torch.from_numpy(x), torch.from_numpy(y)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd import training as T
+    dev = torch.device("cuda", 0)
+    tr = torch.utils.data.TensorDataset(*synthetic_mnist(601, 5000))
+    va = torch.utils.data.TensorDataset(*synthetic_mnist(602, 500))
+    lines = []
+    # warm-up (first kernels, allocator, data loaders): one short untimed run
+    T.SGD(T.modelFactory(SEED=2021).to(dev), gamma=1e-2, aggregate=bz.gm, weight_decay=0.0,
+          noise_var=1e-2, honestSize=45, byzantineSize=5, attack=T.classflip, rounds=1,
+          displayInterval=3, SEED=2021, fixSeed=True, loss_func=torch.nn.CrossEntropyLoss(),
+          train_dataset=tr, validate_dataset=va, device=dev, batchSize=50, verbose=False,
+          eval_train=False)
+    for agg_name, var, layout in (("gm", 1e-2, "rows"), ("gm2", None, "rows"), ("gm2", 1e-2, "rows"),
+                                  ("gm2", None, "panels"), ("median", None, "rows"),
+                                  ("Krum", None, "rows")):
+        base = getattr(bz, agg_name)
+        agg_t = [0.0, 0]
+
+        def timed(X, opts, base=base):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            out = base(X, opts)
+            torch.cuda.synchronize(dev)
+            agg_t[0] += time.perf_counter() - t0
+            agg_t[1] += 1
+            return out
+        timed.__name__ = base.__name__
+        # our gm2 fuses the OMA pre-noise when it is passed itself (training.SGD):
+        # time it through the loop unwrapped when a variance is set, aggregation share n/a
+        agg = base if (agg_name == "gm2" and var is not None) else timed
+        model = T.modelFactory(SEED=2021).to(dev)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        T.SGD(model, gamma=1e-2, aggregate=agg, weight_decay=0.0, noise_var=var, honestSize=45,
+              byzantineSize=5, attack=T.classflip, rounds=1, displayInterval=a.steps, SEED=2021,
+              fixSeed=True, loss_func=torch.nn.CrossEntropyLoss(), train_dataset=tr,
+              validate_dataset=va, device=dev, batchSize=50, verbose=False, layout=layout,
+              eval_train=False)
+        torch.cuda.synchronize(dev)
+        total = time.perf_counter() - t0
+        line = {"what": "training.SGD step (K=50: 45 honest + 5 classflip, MLP d=7850)",
+                "agg": agg_name, "var": var, "layout": layout, "steps": a.steps,
+                "ms_per_step": 1e3 * total / a.steps,
+                "agg_ms_per_step": (1e3 * agg_t[0] / agg_t[1]) if agg_t[1] else None,
+                "note": "includes one validation pass (500 samples) per run"}
+        print(json.dumps(line), flush=True)
+        lines.append(line)
+    if a.out:
+        with open(a.out, "w") as f:
+            for l in lines:
+                f.write(json.dumps(l) + "\n")
+
+
+if __name__ == "__main__":
+    main()
