@@ -290,6 +290,15 @@ def gm(wList, options={}):  # noqa: B006 - the reference's signature (M:131)
 
 
 def _coordinate(wList, fn_name, *extra):
+    if isinstance(wList, ClientPanels):          # the *_panels_f32 kernels (same results)
+        X, ldx, fn_name = wList.data, wList.panel_stride, fn_name.replace("_f32", "_panels_f32")
+        K, d = wList.shape
+        out = torch.empty(d, dtype=torch.float32, device=X.device)
+        ctx = context(X.device)
+        with torch.cuda.device(X.device):
+            _lib.check(getattr(ctx.lib, fn_name)(ctx.handle, X.data_ptr(), K, d, ldx, *extra,
+                                                 out.data_ptr(), _stream_ptr(X.device)), fn_name)
+        return out
     X = _stage(wList)
     X, ldx = _rows(X)
     K, d = X.shape
@@ -319,16 +328,21 @@ def trimmed_mean(wList, options={}):  # noqa: B006 - reference signature (M:189)
 def Krum(wList, options):  # noqa: N802 - reference name (M:197)
     """The row with the smallest sum of squared distances to its honestSize-1
     nearest rows, itself included (M:197-204)."""
-    X = _stage(wList)
-    X, ldx = _rows(X)
-    K, d = X.shape
+    if isinstance(wList, ClientPanels):
+        X, ldx, fn = wList.data, wList.panel_stride, "gm_krum_panels_f32"
+        K, d = wList.shape
+    else:
+        X = _stage(wList)
+        X, ldx = _rows(X)
+        K, d = X.shape
+        fn = "gm_krum_f32"
     out = torch.empty(d, dtype=torch.float32, device=X.device)
     idx = C.c_int64()
     ctx = context(X.device)
     with torch.cuda.device(X.device):
-        _lib.check(ctx.lib.gm_krum_f32(ctx.handle, X.data_ptr(), K, d, ldx,
-                                       int(options["honestSize"]), out.data_ptr(), C.byref(idx),
-                                       _stream_ptr(X.device)), "gm_krum_f32")
+        _lib.check(getattr(ctx.lib, fn)(ctx.handle, X.data_ptr(), K, d, ldx,
+                                        int(options["honestSize"]), out.data_ptr(), C.byref(idx),
+                                        _stream_ptr(X.device)), fn)
     Krum.last_index = idx.value
     return out if wList.device == out.device else out.to(wList.device)
 

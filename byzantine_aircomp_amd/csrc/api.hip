@@ -1109,6 +1109,56 @@ int gm_mean_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, fl
   return GM_OK;
 }
 
+// The coordinate-wise aggregators on client updates in the panel layout: the same
+// kernels with panel addressing (W = gm_panel_width(K) = 2^ws, ldx = panel_stride);
+// results identical to the row-major calls (same per-column reductions).
+static int panel_shift(int64_t K, int64_t panel_stride, int* ws) {
+  const int64_t W = gm_panel_width(K);
+  if (W == 0 || panel_stride < K * W) return GM_ERR_INVALID;
+  int s = 0;
+  while (((int64_t)1 << s) < W) ++s;
+  *ws = s;
+  return GM_OK;
+}
+
+int gm_mean_panels_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t panel_stride,
+                       float* out, void* stream) {
+  int ws = 0;
+  if (!c || !X || !out || K < 1 || d < 0 || panel_shift(K, panel_stride, &ws))
+    return fail(GM_ERR_INVALID, "gm_mean_panels_f32: bad args");
+  if (d == 0) return GM_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(launch_col_mean(X, K, d, panel_stride, out, reinterpret_cast<hipStream_t>(stream), ws));
+  return GM_OK;
+}
+
+int gm_median_panels_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t panel_stride,
+                         float* out, void* stream) {
+  int ws = 0;
+  if (!c || !X || !out || K < 1 || d < 0 || panel_shift(K, panel_stride, &ws))
+    return fail(GM_ERR_INVALID, "gm_median_panels_f32: bad args");
+  if (K > 2048) return fail(GM_ERR_UNSUPPORTED, "gm_median_panels_f32: K <= 2048");
+  if (d == 0) return GM_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(launch_col_select(X, K, d, panel_stride, 0, 0, out, reinterpret_cast<hipStream_t>(stream),
+                           ws));
+  return GM_OK;
+}
+
+int gm_trimmed_mean_panels_f32(gm_ctx* c, const float* X, int64_t K, int64_t d,
+                               int64_t panel_stride, int64_t trim, float* out, void* stream) {
+  int ws = 0;
+  if (!c || !X || !out || K < 1 || d < 0 || trim < 0 || 2 * trim >= K ||
+      panel_shift(K, panel_stride, &ws))
+    return fail(GM_ERR_INVALID, "gm_trimmed_mean_panels_f32: bad args");
+  if (K > 2048) return fail(GM_ERR_UNSUPPORTED, "gm_trimmed_mean_panels_f32: K <= 2048");
+  if (d == 0) return GM_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(launch_col_select(X, K, d, panel_stride, 1, trim, out,
+                           reinterpret_cast<hipStream_t>(stream), ws));
+  return GM_OK;
+}
+
 int gm_honest_variance_f32(gm_ctx* c, const float* X, int64_t honest, int64_t d, int64_t ldx,
                            float* out, void* stream) {
   if (!c || !X || !out || honest < 1 || d < 1 || ldx < d)
@@ -1166,11 +1216,29 @@ int gm_trimmed_mean_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t
   return GM_OK;
 }
 
+static int krum_impl(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, int ws,
+                     int64_t honest, float* out, int64_t* index, void* stream);
+
 int gm_krum_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, int64_t honest,
                 float* out, int64_t* index, void* stream) {
   if (!c || !X || !out || K < 1 || d < 0 || ldx < d || honest < 2 || honest - 1 > K)
     return fail(GM_ERR_INVALID, "gm_krum_f32: bad args (needs 2 <= honestSize <= K+1)");
   if (K > 4096) return fail(GM_ERR_UNSUPPORTED, "gm_krum_f32: K <= 4096");
+  return krum_impl(c, X, K, d, ldx, 0, honest, out, index, stream);
+}
+
+int gm_krum_panels_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t panel_stride,
+                       int64_t honest, float* out, int64_t* index, void* stream) {
+  int ws = 0;
+  if (!c || !X || !out || K < 1 || d < 0 || honest < 2 || honest - 1 > K ||
+      panel_shift(K, panel_stride, &ws))
+    return fail(GM_ERR_INVALID, "gm_krum_panels_f32: bad args (needs 2 <= honestSize <= K+1)");
+  if (K > 4096) return fail(GM_ERR_UNSUPPORTED, "gm_krum_panels_f32: K <= 4096");
+  return krum_impl(c, X, K, d, panel_stride, ws, honest, out, index, stream);
+}
+
+static int krum_impl(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, int ws,
+                     int64_t honest, float* out, int64_t* index, void* stream) {
   HIPCHK(hipSetDevice(c->device));
   WsOrder order(c, reinterpret_cast<hipStream_t>(stream));
   HIPCHK(order.err);
@@ -1181,7 +1249,7 @@ int gm_krum_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, in
   if (rc) return rc;
   int64_t* didx = reinterpret_cast<int64_t*>(w.u);
   HIPCHK(launch_krum(X, K, d, ldx, honest - 1, w.G, reinterpret_cast<double*>(w.gslab), w.alpha,
-                     out, didx, reinterpret_cast<hipStream_t>(stream)));
+                     out, didx, reinterpret_cast<hipStream_t>(stream), ws));
   if (index) {
     HIPCHK(hipMemcpyAsync(index, didx, sizeof(int64_t), hipMemcpyDeviceToHost,
                           reinterpret_cast<hipStream_t>(stream)));

@@ -13,18 +13,28 @@
 
 namespace gmk {
 
+// Element (row k, column j) of a client matrix: row-major [K][ldx] (ws = 0), or the
+// panel layout [ceil(d/W)][K][W] with W = 2^ws and ldx = the panel stride.  A group of
+// 4 columns starting at a multiple of 4 never straddles a panel (W % 4 == 0), so the
+// float4 paths below read it as one vector either way.
+__device__ __forceinline__ const float* elem(const float* X, int64_t ldx, int ws, int64_t k,
+                                             int64_t j) {
+  return ws ? X + (j >> ws) * ldx + (k << ws) + (j & ((1 << ws) - 1)) : X + k * ldx + j;
+}
+
 // mean: W consecutive columns per thread (W = 4: one float4 per row, 1 KiB per wave
 // instruction), 8 rows' loads in flight, each column summed in fp64 in row order
 // and rounded once (the same sums for every W).
 template <int W>
 __global__ void __launch_bounds__(256) col_mean(const float* __restrict__ X, int64_t K, int64_t d,
-                                                int64_t ldx, float* __restrict__ out) {
+                                                int64_t ldx, int ws, float* __restrict__ out) {
   typedef float fv __attribute__((ext_vector_type(W)));
   constexpr int U = 8;
   const int64_t G = d / W;            // W > 1: d % W == 0 (checked by the launcher)
+  const int64_t rs = ws ? ((int64_t)1 << ws) : ldx;   // row stride
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G;
        g += (int64_t)gridDim.x * blockDim.x) {
-    const float* col = X + g * W;
+    const float* col = elem(X, ldx, ws, 0, g * W);
     double s[W];
 #pragma unroll
     for (int v = 0; v < W; ++v) s[v] = 0.0;
@@ -33,14 +43,14 @@ __global__ void __launch_bounds__(256) col_mean(const float* __restrict__ X, int
       fv x[U];
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        x[u] = __builtin_nontemporal_load(reinterpret_cast<const fv*>(col + (k + u) * ldx));
+        x[u] = __builtin_nontemporal_load(reinterpret_cast<const fv*>(col + (k + u) * rs));
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int v = 0; v < W; ++v) s[v] += (double)x[u][v];
     }
     for (; k < K; ++k) {
-      const fv x = *reinterpret_cast<const fv*>(col + k * ldx);
+      const fv x = *reinterpret_cast<const fv*>(col + k * rs);
 #pragma unroll
       for (int v = 0; v < W; ++v) s[v] += (double)x[v];
     }
@@ -375,8 +385,8 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
 
 template <int R, int C, int NWV>
 __global__ void __launch_bounds__(NWV * 64) col_select(const float* __restrict__ X, int64_t K,
-                                                  int64_t d, int64_t ldx, int mode, int64_t b,
-                                                  int vec4, float* __restrict__ out) {
+                                                  int64_t d, int64_t ldx, int ws, int mode,
+                                                  int64_t b, int vec4, float* __restrict__ out) {
   __shared__ float tile[64 * R][C + 1];
   const int64_t ntiles = (d + C - 1) / C;
   // XCD-aware: blocks bid and bid+8 run on the same XCD; give them adjacent tiles
@@ -398,7 +408,7 @@ __global__ void __launch_bounds__(NWV * 64) col_select(const float* __restrict__
         const int64_t k = base + (int64_t)u * RPI;
         buf[u] = f4{0.f, 0.f, 0.f, 0.f};
         if (k < K) {
-          const float* src = X + k * ldx + col;
+          const float* src = elem(X, ldx, ws, k, col);
           if (vec) {
             buf[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src));
           } else {
@@ -500,7 +510,7 @@ constexpr int kPDT = 512;  // pair_dist threads per block
 
 template <bool VEC>
 __global__ void __launch_bounds__(kPDT) pair_dist(const float* __restrict__ X, int64_t K,
-                                                 int64_t d, int64_t ldx, int64_t chunk,
+                                                 int64_t d, int64_t ldx, int ws, int64_t chunk,
                                                  double* __restrict__ part) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) float sA[kPC][kPT + 4];
@@ -529,7 +539,7 @@ __global__ void __launch_bounds__(kPDT) pair_dist(const float* __restrict__ X, i
         const int64_t row = (t ? bj : bi) * kPT + r;
         f4 v = {0.f, 0.f, 0.f, 0.f};
         if (row < K && col < ce) {
-          const float* src = X + row * ldx + col;
+          const float* src = elem(X, ldx, ws, row, col);
           if (VEC && col + 4 <= ce) {
             v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src));
           } else {
@@ -653,12 +663,13 @@ __global__ void __launch_bounds__(64) krum_argmin(const double* __restrict__ sco
 
 // Krum, step 4: out = row *index, grid-wide copy.
 __global__ void __launch_bounds__(256) copy_row(const float* __restrict__ X, int64_t d,
-                                                int64_t ldx, const int64_t* __restrict__ index,
+                                                int64_t ldx, int ws,
+                                                const int64_t* __restrict__ index,
                                                 float* __restrict__ out) {
-  const float* src = X + *index * ldx;
+  const int64_t k = *index;
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < d;
        c += (int64_t)gridDim.x * blockDim.x)
-    out[c] = src[c];
+    out[c] = *elem(X, ldx, ws, k, c);
 }
 
 static int grid_cols(int64_t d) {
@@ -667,21 +678,21 @@ static int grid_cols(int64_t d) {
 }
 
 hipError_t launch_col_mean(const float* X, int64_t K, int64_t d, int64_t ldx, float* out,
-                           hipStream_t s) {
+                           hipStream_t s, int ws) {
   const bool vec4 = reinterpret_cast<uintptr_t>(X) % 16 == 0 && ldx % 4 == 0 && d % 4 == 0;
   if (vec4)
-    hipLaunchKernelGGL(col_mean<4>, dim3(grid_cols(d / 4)), dim3(256), 0, s, X, K, d, ldx, out);
+    hipLaunchKernelGGL(col_mean<4>, dim3(grid_cols(d / 4)), dim3(256), 0, s, X, K, d, ldx, ws, out);
   else
-    hipLaunchKernelGGL(col_mean<1>, dim3(grid_cols(d)), dim3(256), 0, s, X, K, d, ldx, out);
+    hipLaunchKernelGGL(col_mean<1>, dim3(grid_cols(d)), dim3(256), 0, s, X, K, d, ldx, ws, out);
   return hipGetLastError();
 }
 
 hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, int mode,
-                             int64_t b, float* out, hipStream_t s) {
+                             int64_t b, float* out, hipStream_t s, int ws) {
   const int vec4 = reinterpret_cast<uintptr_t>(X) % 16 == 0 && ldx % 4 == 0;
 #define GMK_SEL(R, C, NWV)                                                                    \
   hipLaunchKernelGGL((col_select<R, C, NWV>), dim3((unsigned)((d + C - 1) / C)), dim3(NWV * 64), 0, \
-                     s, X, K, d, ldx, mode, b, vec4, out)
+                     s, X, K, d, ldx, ws, mode, b, vec4, out)
   // K <= 1024: 8 waves per 69.6-KB tile (one column pair each) so that the CU holds
   // 4 waves per SIMD (the LDS allows 2 tiles) instead of 2
   if (K <= 64) GMK_SEL(1, 32, 4);
@@ -725,17 +736,18 @@ int64_t krum_slices(int64_t K, int64_t d) {
 }
 
 hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t kk, double* D,
-                       double* part, double* score, float* out, int64_t* index, hipStream_t s) {
+                       double* part, double* score, float* out, int64_t* index, hipStream_t s,
+                       int ws) {
   const int64_t nT = (K + kPT - 1) / kPT, pairs = nT * (nT + 1) / 2;
   const int64_t S = krum_slices(K, d);
   const int64_t chunk = ((d + S - 1) / S + kPC - 1) / kPC * kPC;
   const bool vec = reinterpret_cast<uintptr_t>(X) % 16 == 0 && ldx % 4 == 0;
   if (vec)
     hipLaunchKernelGGL(pair_dist<true>, dim3((unsigned)pairs, (unsigned)S), dim3(kPDT), 0, s, X, K,
-                       d, ldx, chunk, part);
+                       d, ldx, ws, chunk, part);
   else
     hipLaunchKernelGGL(pair_dist<false>, dim3((unsigned)pairs, (unsigned)S), dim3(kPDT), 0, s, X,
-                       K, d, ldx, chunk, part);
+                       K, d, ldx, ws, chunk, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(pair_reduce, dim3((unsigned)((K * K + 63) / 64)), dim3(256), 0, s, part, S, K,
@@ -745,7 +757,7 @@ hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_
   hipLaunchKernelGGL(krum_argmin, dim3(1), dim3(64), 0, s, score, K, index);
   if (d > 0)
     hipLaunchKernelGGL(copy_row, dim3((unsigned)std::min<int64_t>((d + 255) / 256, 2048)),
-                       dim3(256), 0, s, X, d, ldx, index, out);
+                       dim3(256), 0, s, X, d, ldx, ws, index, out);
   return hipGetLastError();
 }
 

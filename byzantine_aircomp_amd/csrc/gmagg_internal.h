@@ -151,10 +151,11 @@ hipError_t launch_gram_solve(const double* G, int KP, int64_t K, int64_t maxiter
                              hipStream_t s);
 
 // Other aggregators (coordinate.hip).
+// ws > 0: X in the panel layout [ceil(d/W)][K][W], W = 2^ws, ldx = the panel stride.
 hipError_t launch_col_mean(const float* X, int64_t K, int64_t d, int64_t ldx, float* out,
-                           hipStream_t s);
+                           hipStream_t s, int ws = 0);
 hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, int mode,
-                             int64_t b, float* out, hipStream_t s);
+                             int64_t b, float* out, hipStream_t s, int ws = 0);
 // getVarience (M:127-129): one streaming pass, part[nb] fp64 block partials.
 int honest_var_blocks(int64_t d, int num_cu);
 hipError_t launch_honest_var(const float* X, int64_t H, int64_t d, int64_t ldx, int wshift,
@@ -162,7 +163,8 @@ hipError_t launch_honest_var(const float* X, int64_t H, int64_t d, int64_t ldx, 
 // Krum: D [K][K] fp64, part [krum_slices(K, d)][K][K] fp64, score [K] fp64.
 int64_t krum_slices(int64_t K, int64_t d);
 hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t kk, double* D,
-                       double* part, double* score, float* out, int64_t* index, hipStream_t s);
+                       double* part, double* score, float* out, int64_t* index, hipStream_t s,
+                       int ws = 0);
 
 // OMA / synthetic fills (oma.hip).
 hipError_t launch_oma_apply(float* X, int64_t K, int64_t d, int64_t ldx, const float* hr,

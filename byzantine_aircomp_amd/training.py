@@ -181,7 +181,7 @@ def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # 
         fixSeed=False, loss_func=None, train_dataset=None, validate_dataset=None, device=None,
         batchSize=None, num_classes=10, verbose=True, layout="rows", eval_train=True, **kw):
     """Federated SGD with K = honest + Byzantine simulated clients (M:226-372).
-    layout="panels" keeps the client matrix in the panel layout (gm / gm2 only).
+    layout="panels" keeps the client matrix in the panel layout (every aggregator).
     EMNIST_Air_weight.py's variant: num_classes=62 (its MLP(784, 62) and 61 - y
     relabel, E:101, E:321) and eval_train=False (train loss / accuracy recorded as
     0, 0, E:273-274, E:364-365)."""
@@ -214,9 +214,9 @@ def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # 
         _log(f"[0/{rounds}] train: loss={tl:.4f} acc={ta:.4f} val: loss={vl:.4f} acc={va:.4f}")
 
     attack_name = attack.__name__ if attack is not None else None
-    if layout == "panels" and (aggregate.__name__ not in ("gm", "gm2") or attack_name == "weightflip"):
-        raise ValueError("layout='panels' supports the gm / gm2 aggregators and the classflip / "
-                         "dataflip attacks (weightflip and the coordinate-wise aggregators need rows)")
+    if layout == "panels" and attack_name == "weightflip":
+        raise ValueError("layout='panels' supports the classflip / dataflip attacks (weightflip "
+                         "rewrites whole rows: use layout='rows')")
     clients = ClientUpdates(model, K, layout=layout)
     params = clients.params
     is_gm = aggregate.__name__ == "gm"

@@ -191,6 +191,16 @@ int gm_trimmed_mean_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64
                         int64_t trim, float* out, void* stream);
 int gm_krum_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t ldx,
                 int64_t honest_size, float* out, int64_t* index, void* stream);
+/* The same four on client updates in the panel layout (GM_LAYOUT_PANELS: X as
+ * [ceil(d/W)][K][W], W = gm_panel_width(K), panel_stride >= K*W): identical results. */
+int gm_mean_panels_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t panel_stride,
+                       float* out, void* stream);
+int gm_median_panels_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t panel_stride,
+                         float* out, void* stream);
+int gm_trimmed_mean_panels_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d,
+                               int64_t panel_stride, int64_t trim, float* out, void* stream);
+int gm_krum_panels_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t panel_stride,
+                       int64_t honest_size, float* out, int64_t* index, void* stream);
 
 /* getVarience(w_local, honestSize) (MNIST_Air_weight.py:127-129): the mean over the
  * first `honest` rows of ||x_k - mean||^2, written as ONE fp32 value to the device

@@ -112,3 +112,24 @@ def test_krum_strided_rows():
     X = base[:, 3:520]                                # ldx = 530, unaligned start
     out = bz.Krum(X.cuda(), {"honestSize": 30})
     assert torch.equal(out.cpu(), orc.krum(X.contiguous(), {"honestSize": 30}))
+
+
+@pytest.mark.parametrize("K,d", [(20, 640), (50, 7850), (65, 257), (256, 300), (300, 513),
+                                 (1000, 200), (1025, 33)])
+def test_coordinate_aggregators_on_panels(K, d):
+    """mean / median / trimmed_mean / Krum on a ClientPanels == on the row-major matrix
+    (the same kernels with panel addressing: bit-identical)."""
+    import byzantine_aircomp_amd as bz
+    g = torch.Generator().manual_seed(K * 11 + d)
+    X = torch.randn(K, d, generator=g)
+    X[:, ::5] = torch.round(4 * X[:, ::5]) / 4
+    Xc = X.cuda()
+    P = bz.ClientPanels.from_rows(Xc)
+    for f in (bz.mean, bz.median, bz.trimmed_mean):
+        assert torch.equal(f(P, {}), f(Xc, {})), f.__name__
+    if K <= 1024:
+        honest = max(2, int(0.8 * K))
+        a = bz.Krum(Xc, {"honestSize": honest})
+        ia = bz.aggregators.Krum.last_index
+        b = bz.Krum(P, {"honestSize": honest})
+        assert bz.aggregators.Krum.last_index == ia and torch.equal(a, b)
