@@ -467,10 +467,12 @@ def test_pre_oma_equals_oma_then_gm2(K, d, layout, algo):
     assert (ra.iters, ra.algo) == (rb.iters, rb.algo)
 
 
-@pytest.mark.parametrize("layout", ["rows", "panels"])
-def test_batched_pre_oma_equals_oma_then_gm2(layout):
+@pytest.mark.parametrize("layout,d", [("rows", 10000), ("panels", 10000), ("rows", 1001),
+                                      ("panels", 1001)])
+def test_batched_pre_oma_equals_oma_then_gm2(layout, d):
+    """(rows at d % 4 != 0 take the float1 tile: the standalone batched OMA runs first)"""
     from byzantine_aircomp_amd.batched import ProblemPanels, gm2_batched, oma_batched
-    P, K, d = 6, 50, 10000
+    P, K = 6, 50
     g = torch.Generator().manual_seed(3)
     X = (0.05 * torch.randn(P, K, d, generator=g)).cuda()
     g0 = (0.01 * torch.randn(P, d, generator=g)).cuda()
