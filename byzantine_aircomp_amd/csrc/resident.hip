@@ -150,7 +150,6 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   __shared__ float s_coef[KMAX];
   __shared__ double s_d2[KMAX];
   __shared__ double s_r[KMAX];
-  __shared__ double s_tot[2];
   __shared__ double s_wp[2];
   __shared__ float s_h2[KMAX];
   __shared__ float s_nd;
@@ -272,6 +271,11 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   int64_t it = 0;
   double last_mv = NAN;
   int conv = 0;
+  // the finisher column's AirComp noise draw of the coming pass: data-independent, so it
+  // is drawn right after the previous pass is published, while the other blocks'
+  // partials are still on their way (off the iteration's critical path)
+  const bool col_noise = a.has_noise && a.mode == 1 && fin;
+  float nz = col_noise ? normal1(a.seed, kStreamNoise, 0, (uint64_t)gj) : 0.f;
 #ifdef GMK_RES_PROF
   uint64_t prof_[6] = {0, 0, 0, 0, 0, 0};
   uint64_t prev_ = __builtin_amdgcn_s_memrealtime();
@@ -322,17 +326,12 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         else if (cc < nk) s_r[cc - K] = sum;
         else s_wp[cc - nk] = sum;
       }
-      __syncthreads();
-      if (tid == 0) {
-        s_tot[0] = s_wp[0];
-        s_tot[1] = s_wp[1];
-      }
-      __syncthreads();
+      __syncthreads();   // (s_wp is read in place: its next write follows this iteration's barriers)
     }
     RES_T(0)
     // (2) tol test of the pass that produced g_it (M:180-183)
     if (it >= 1) {
-      const float mv = (float)sqrt(s_tot[0]);
+      const float mv = (float)sqrt(s_wp[0]);
       last_mv = (double)mv;
       if (mv <= a.tol) { conv = 1; break; }
     }
@@ -349,7 +348,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
           if (kv) s_coef[k] = (float)(wk / W);
           if (lane == 0) s_anoise = 0.f;
         } else {
-          const float s = sqrtf((float)(s_tot[1] / (double)d));      // M:146
+          const float s = sqrtf((float)(s_wp[1] / (double)d));      // M:146
           const float thr = (s * s) * 500.0f;                         // M:152
           const double s2 = (double)s * (double)s;
           double ck = 0.0;
@@ -387,7 +386,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         s_coef[k] = (float)((1.0 / (double)clamp_dist(s_d2[k], a.eps)) / W);
       if (tid == 0) s_anoise = 0.f;
     } else {
-      const float s = sqrtf((float)(s_tot[1] / (double)d));      // M:146
+      const float s = sqrtf((float)(s_wp[1] / (double)d));      // M:146
       const float thr = (s * s) * 500.0f;                         // M:152
       const double s2 = (double)s * (double)s;
       double csum = 0.0;
@@ -450,8 +449,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
 #pragma unroll
         for (int ww = 0; ww < NW; ++ww) sum += s_red[ww][tid];
         gnew = sum;
-        if (a.has_noise && a.mode == 1)
-          gnew = fmaf(s_anoise, normal1(a.seed, kStreamNoise, (uint64_t)it, (uint64_t)gj), gnew);
+        if (col_noise) gnew = fmaf(s_anoise, nz, gnew);
         const float diff = gcur - gnew;
         mvp = diff * diff;
         gnp = gnew * gnew;
@@ -488,6 +486,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
     }
     RES_T(3)
     publish(it + 1, racc, nullptr, mvp, gnp);
+    if (col_noise) nz = normal1(a.seed, kStreamNoise, (uint64_t)(it + 1), (uint64_t)gj);
     RES_T(4)
   }
 #ifdef GMK_RES_PROF
