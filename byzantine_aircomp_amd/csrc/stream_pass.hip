@@ -183,8 +183,10 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
       const int64_t k = rg + (int64_t)NRG * i;
       float z[4];
       normal4_hw(a.oma_seed, kStreamOmaNoise, (uint64_t)k, (uint64_t)(a.col_off + col) >> 2, z);
+      // (the padding columns of a partial last group stay 0: they enter the distances)
 #pragma unroll
-      for (int v = 0; v < V; ++v) t.x[i][v] = oma_noisy(t.x[i][v], osc[i], z[v]);
+      for (int v = 0; v < V; ++v)
+        if (col + v < d) t.x[i][v] = oma_noisy(t.x[i][v], osc[i], z[v]);
       float* dst;
       if constexpr (PANEL)
         dst = const_cast<float*>(a.X) + ch * a.panel_stride + k * J + c * V;
