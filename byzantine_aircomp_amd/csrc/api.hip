@@ -973,10 +973,12 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
   const int64_t nch = (d + J - 1) / J;
   // blocks per problem: the grid is OVERSUB rounds of co-resident blocks, so that the
   // iterations where only the slowest problems are still active (the others exit at
-  // their `done` flag) still spread over the chip (GMAGG_BATCH_OVERSUB: A/B)
+  // their `done` flag) still spread over the chip.  C5 on ProblemPanels: 8 rounds
+  // 40.7-41.7k vs 2 rounds 39.7-39.9k problems/s (profiles/r2_c5_oversub.txt;
+  // GMAGG_BATCH_OVERSUB: A/B)
   static const int oversub = [] {
     const char* e = getenv("GMAGG_BATCH_OVERSUB");
-    return e && atoi(e) > 0 ? atoi(e) : 2;
+    return e && atoi(e) > 0 ? atoi(e) : 8;
   }();
   const int64_t target = (int64_t)c->num_cu * pass_blocks_per_cu(cfg, 0) * oversub;
   const int nbp = (int)std::max<int64_t>(1, std::min<int64_t>(nch, (target + P - 1) / P));
