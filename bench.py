@@ -96,6 +96,9 @@ def parse():
                         "the per-rank time of the N=P run minus the cross-GPU all-reduce latency. "
                         "Convergence uses the shard's sums only, so iters may differ from N=P.")
     p.add_argument("--problems", type=int, default=4096, help="c5: problems per sweep")
+    p.add_argument("--c5-batch", type=int, default=1024,
+                   help="c5: problems per batched call (small batches keep a group's passes "
+                        "inside the 256 MiB Infinity Cache)")
     p.add_argument("--reading", default="prenoise", choices=["prenoise", "aircomp"],
                    help="c5: var > 0 as the reference's `--agg gm2 --var v` (OMA pre-noise, then "
                         "gm2; M:351-353) or as the AirComp gm aggregator (M:131-160)")
@@ -229,7 +232,7 @@ def run_c5(args, json_out):
     ctx = bz.context(dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
     per_var = args.problems // len(C5_VARS)
-    chunk = min(1024, per_var)
+    chunk = max(1, min(args.c5_batch, per_var))
     # layout: the batched problems in the panel layout (ProblemPanels: every chunk one
     # contiguous block, as for C3) unless --layout rows; the panels are packed from the
     # row-major fill, untimed
@@ -333,7 +336,7 @@ def run_c5(args, json_out):
                                    " (OMA pre-noise then gm2, M:351-353; the pre-noise fused "
                                    "into gm2's first pass)")
                                   if args.reading == "prenoise" else " (AirComp gm for var > 0)"),
-                   "K": K, "d": d, "problems": n_prob, "mean_iters": mean_it,
+                   "K": K, "d": d, "problems": n_prob, "mean_iters": mean_it, "batch": chunk,
                    "parallelism": "batched (one launch per pass covers every problem of a group)",
                    "layout": "panels (ProblemPanels)" if use_panels else "rows",
                    "groups": {str(k): {"problems_per_s": v["problems"] / v["seconds"],
