@@ -71,6 +71,8 @@ struct gm_ctx {
   hipEvent_t ws_ev = nullptr;
   hipStream_t ws_stream = nullptr;
   bool ws_pending = false;
+  float* stage = nullptr;   // panel copy of a row-major client matrix (gm_weiszfeld_f32)
+  size_t stage_bytes = 0;
 };
 
 namespace {
@@ -470,6 +472,7 @@ int gm_ctx_destroy(gm_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->ws) (void)hipFree(c->ws);
+  if (c->stage) (void)hipFree(c->stage);
   if (c->host) (void)hipHostFree(c->host);
   for (auto e : c->poll_ev)
     if (e) (void)hipEventDestroy(e);
@@ -680,6 +683,39 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   }
   if (algo == GM_ALGO_RESIDENT)
     return fail(GM_ERR_UNSUPPORTED, "resident kernel: problem too large, sharded or host noise");
+  // Row-major AirComp gm over many passes (the reference's `gm`: 1000 iterations, never
+  // meeting tol; M:131-160) on a large client matrix: pack the panel layout once into a
+  // context-owned buffer (one read + one write of X) and stream every pass from it.  Rows
+  // stream at 79-80 % of HBM against 85-87 % on panels (C3 STEP 6.87-6.99 vs 6.35-6.47 ms),
+  // so the copy pays for itself after ~35 passes.  Results equal the row-major passes' bit
+  // for bit where both run the same tile (K outside 32 < K <= 64 and 128 < K <= 256, V = 4).
+  // If the buffer cannot be allocated the rows are streamed.  GMAGG_STAGE_PANELS=0: off.
+  if (!panels && algo == GM_ALGO_AUTO && !sharded && !c->comm && !c->ar_fn &&
+      o->mode == GM_MODE_AIRCOMP && o->has_noise && !host_noise_req && o->maxiter >= 64 &&
+      K * d >= ((int64_t)1 << 24)) {
+    static const bool stage_on = [] {
+      const char* e = getenv("GMAGG_STAGE_PANELS");
+      return !(e && atoi(e) == 0);
+    }();
+    const int64_t W = gm_panel_width(K);
+    if (stage_on && W > 0 && K * W * 4 <= 0x7fffffff) {
+      const size_t bytes = sizeof(float) * (size_t)((d + W - 1) / W) * (size_t)(K * W);
+      if (bytes > c->stage_bytes) {
+        if (c->stage) HIPCHK(hipFree(c->stage));   // (hipFree waits for queued work)
+        c->stage = nullptr;
+        c->stage_bytes = 0;
+        if (hipMalloc(&c->stage, bytes) == hipSuccess) c->stage_bytes = bytes;
+        else { (void)hipGetLastError(); c->stage = nullptr; }
+      }
+      if (c->stage) {
+        HIPCHK(launch_rows_to_panels(X, K, d, ldx, c->stage, W, K * W, s));
+        gm_opts o2 = *o;
+        o2.layout = GM_LAYOUT_PANELS;
+        o2.algo = GM_ALGO_STREAM;
+        return gm_weiszfeld_f32(c, c->stage, K, d, K * W, guess0, out, &o2, res, stream);
+      }
+    }
+  }
   if (panels) {
     // cfg fixed above
   } else if (algo == GM_ALGO_AUTO || algo == GM_ALGO_STREAM) {

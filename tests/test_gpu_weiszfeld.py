@@ -190,6 +190,30 @@ def test_gm_philox_reproducible_and_close_to_ideal():
     assert rel_l2(a.cpu().numpy(), ideal.cpu().numpy()) < 0.05
 
 
+@pytest.mark.parametrize("K,d,exact", [(300, 1 << 20, True), (50, 1 << 22, False),
+                                         (1000, 65537, False)])
+def test_gm_rows_staged_as_panels(K, d, exact):
+    """Row-major AirComp gm with >= 64 passes on K*d >= 2^24 packs a panel copy once and
+    streams every pass from it (api.hip gm_weiszfeld_f32).  Against the row-major passes
+    (algo="stream"): bit-identical where both run the same tile (K=300, d % 4 == 0),
+    relative L2 1e-5 otherwise (K=50: another tile; d odd: float1 rows); the same
+    iteration count (gm runs to maxiter).  Sizes beyond the register-resident kernel."""
+    g = torch.Generator().manual_seed(K + d)
+    X = (0.05 * torch.randn(K, d, generator=g)).cuda()
+    X[: K // 10] += 0.3
+    g0 = (0.01 * torch.randn(d, generator=g)).cuda()
+    o = {"maxiter": 64, "tol": 1e-5, "noise_var": 1e-2, "P_max": 1, "seed": 99, "guess": g0}
+    a = bz().gm(X, o)
+    ra = bz().aggregators.last_result
+    b = bz().gm(X, dict(o, algo="stream"))
+    rb = bz().aggregators.last_result
+    assert (ra.iters, ra.algo) == (rb.iters, rb.algo) == (64, "stream")
+    if exact:
+        assert torch.equal(a, b)
+    else:
+        assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 1e-5
+
+
 @pytest.mark.parametrize("K", [1, 2, 16, 17, 33, 64, 65, 129, 257, 513, 1000, 1025, 2049])
 @pytest.mark.parametrize("d", [1, 6, 4099])
 def test_gm2_shapes_vs_oracle(K, d):

@@ -78,6 +78,27 @@ def main():
               "s_per_aggregation_at_1000_it_est": per * 1001})
         del P
 
+    if want("a2r"):
+        # gm (AirComp) at the C3 shape on the row-major [K, d] input the reference hands
+        # over: >= 64 passes pack a panel copy once (GMAGG_STAGE_PANELS=0: the rows are
+        # streamed instead; run both for the A/B); 200 iterations per call
+        K, d = 1000, 11_000_000
+        X = torch.empty(K, d, device="cuda")
+        fill(ctx, X, 200, 20211)
+        g0 = 0.01 * torch.randn(d, device="cuda")
+        ctx.pass_timing(True)
+        t = timed(lambda: bz.gm(X, {"maxiter": 200, "noise_var": 1e-2, "seed": 7, "guess": g0}),
+                  reps=2)
+        ms, n = ctx.pass_timing(False)
+        per = ms / 1e3 / max(n, 1)
+        import os
+        emit({"row": "a2r", "what": "gm AirComp, C3 shape, rows input, 200 iterations",
+              "stage_panels": os.environ.get("GMAGG_STAGE_PANELS", "1") != "0",
+              "K": K, "d": d, "iters": bz.aggregators.last_result.iters,
+              "s_per_call_200it": t, "pass_us": per * 1e6, "frac": 4.0 * K * d / per / HBM,
+              "s_per_aggregation_at_1000_it_est": t * 1001 / 201})
+        del X
+
     if want("a4"):
         K, d = 1000, 11_000_000
         X = torch.zeros(K, d, device="cuda")
