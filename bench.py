@@ -319,6 +319,7 @@ def run_c5(args, json_out):
                "groups": {str(k): {"problems_per_s": v["problems"] / v["seconds"],
                                    "mean_iters": v["iters"] / v["problems"]}
                           for k, v in a_groups.items()}}
+    traffic, traffic_src = pmc_traffic("c5", "panels" if use_panels else "rows")
     cpu = None
     if not args.no_cpu:
         cpu = c5_cpu_baseline(groups[0][3][0], groups[0][4][0], mean_it, n_prob, args.cpu_budget)
@@ -343,7 +344,11 @@ def run_c5(args, json_out):
                                        "mean_iters": v["iters"] / v["problems"]}
                               for k, v in per_group.items()}},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+                     "traffic_unit": "GB per batched STEP launch with every problem of a "
+                                     f"{chunk}-problem group active (PMC of the AirComp reading)",
+                     "traffic_algorithmic": chunk * 4.0 * K * d / 1e9 if traffic else None,
+                     "traffic_source": traffic_src,
                      "kernel": "weiszfeld_pass (batched STEP, blockIdx.y = problem)",
                      "launches_timed": launches, "avg_launch_us": 1e3 * pass_ms / max(launches, 1),
                      "algorithmic_bytes": "4*K*d per problem per Weiszfeld iteration (sum over "
