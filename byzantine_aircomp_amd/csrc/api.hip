@@ -978,6 +978,36 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   WsOrder order(c, s);
   HIPCHK(order.err);
+  // Row-major AirComp problems over >= 64 passes: pack them once into the context's panel
+  // buffer and stream every pass from it, as gm_weiszfeld_f32 does (C5 AirComp reading on
+  // rows: every problem runs all 1000 iterations).  GMAGG_STAGE_PANELS=0: off.
+  if (!panels && o->mode == GM_MODE_AIRCOMP && o->maxiter >= 64 &&
+      P * K * d >= ((int64_t)1 << 24)) {
+    static const bool stage_on = [] {
+      const char* e = getenv("GMAGG_STAGE_PANELS");
+      return !(e && atoi(e) == 0);
+    }();
+    const int64_t W = gm_panel_width(K);
+    if (stage_on && W > 0 && K * W * 4 <= 0x7fffffff) {
+      const int64_t pst = (d + W - 1) / W * K * W;   // problem stride (floats)
+      const size_t bytes = sizeof(float) * (size_t)(P * pst);
+      if (bytes > c->stage_bytes) {
+        if (c->stage) HIPCHK(hipFree(c->stage));   // (hipFree waits for queued work)
+        c->stage = nullptr;
+        c->stage_bytes = 0;
+        if (hipMalloc(&c->stage, bytes) == hipSuccess) c->stage_bytes = bytes;
+        else { (void)hipGetLastError(); c->stage = nullptr; }
+      }
+      if (c->stage) {
+        for (int64_t p = 0; p < P; ++p)
+          HIPCHK(launch_rows_to_panels(X + p * ldp, K, d, ldx, c->stage + p * pst, W, K * W, s));
+        gm_opts o2 = *o;
+        o2.layout = GM_LAYOUT_PANELS;
+        return gm_weiszfeld_batched_f32(c, c->stage, P, K, d, K * W, pst, guess0, ldg, out, ldo,
+                                        &o2, results, stream);
+      }
+    }
+  }
   // pre_oma (the reference's `--agg gm2 --var v` pre-noise, M:351-352): fused into the
   // INIT pass when the tile takes float4 groups, else the standalone batched OMA first;
   // problem p keyed pre_oma_seed + p * kSeedStride either way

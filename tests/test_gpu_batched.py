@@ -126,3 +126,26 @@ def test_batched_panels_match_rows(K, d, agg):
         for p in range(P):
             assert rel_l2(b[p].cpu().numpy(), a[p].cpu().numpy()) <= tol
             assert abs(ra[p].iters - rb[p].iters) <= 1
+
+
+def test_batched_gm_rows_staged_as_panels():
+    """Row-major batched AirComp gm over >= 64 passes (P*K*d >= 2^24) is packed once into
+    the context's panel buffer (api.hip gm_weiszfeld_batched_f32): bit-identical to the
+    ProblemPanels call, and each problem equal to rounding to a single row-major
+    `gm(..., algo="stream")` call with the problem's seed (not staged)."""
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd.batched import SEED_STRIDE, ProblemPanels, gm_batched
+    P, K, d = 4, 300, 16_384
+    g = torch.Generator().manual_seed(31)
+    X = (0.05 * torch.randn(P, K, d, generator=g)).cuda()
+    X[:, : K // 10] += 0.3
+    g0 = (0.01 * torch.randn(P, d, generator=g)).cuda()
+    opts = {"maxiter": 64, "tol": 1e-5, "noise_var": 1e-2, "seed": 11, "guess": g0}
+    a, ra = gm_batched(X, dict(opts))
+    b, rb = gm_batched(ProblemPanels.from_rows(X), dict(opts))
+    assert torch.equal(a, b)
+    assert [r.iters for r in ra] == [r.iters for r in rb] == [64] * P
+    for i in range(P):
+        single = bz.gm(X[i], dict(opts, guess=g0[i], seed=(11 + i * SEED_STRIDE) % 2 ** 64,
+                                  algo="stream"))
+        assert rel_l2(a[i].cpu().numpy(), single.cpu().numpy()) <= 1e-5
