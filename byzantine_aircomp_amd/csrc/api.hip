@@ -97,6 +97,31 @@ struct WsOrder {
   }
 };
 
+// The context's panel copy of a row-major client matrix (gm_weiszfeld_f32 /
+// gm_weiszfeld_batched_f32 stage row-major AirComp inputs into it).  GMAGG_STAGE_PANELS=0
+// turns staging off.  Returns false (and streams the rows) when the buffer cannot be had.
+bool stage_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("GMAGG_STAGE_PANELS");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+bool ensure_stage(gm_ctx* c, size_t bytes) {
+  if (bytes <= c->stage_bytes) return true;
+  if (c->stage) (void)hipFree(c->stage);   // (hipFree waits for queued work)
+  c->stage = nullptr;
+  c->stage_bytes = 0;
+  if (hipMalloc(&c->stage, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    c->stage = nullptr;
+    return false;
+  }
+  c->stage_bytes = bytes;
+  return true;
+}
+
 struct Workspace {
   KState* st;
   double* sums;
@@ -689,25 +714,13 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   // stream at 79-80 % of HBM against 85-87 % on panels (C3 STEP 6.87-6.99 vs 6.35-6.47 ms),
   // so the copy pays for itself after ~35 passes.  Results equal the row-major passes' bit
   // for bit where both run the same tile (K outside 32 < K <= 64 and 128 < K <= 256, V = 4).
-  // If the buffer cannot be allocated the rows are streamed.  GMAGG_STAGE_PANELS=0: off.
+  // If the buffer cannot be allocated the rows are streamed (ensure_stage).
   if (!panels && algo == GM_ALGO_AUTO && !sharded && !c->comm && !c->ar_fn &&
       o->mode == GM_MODE_AIRCOMP && o->has_noise && !host_noise_req && o->maxiter >= 64 &&
       K * d >= ((int64_t)1 << 24)) {
-    static const bool stage_on = [] {
-      const char* e = getenv("GMAGG_STAGE_PANELS");
-      return !(e && atoi(e) == 0);
-    }();
     const int64_t W = gm_panel_width(K);
-    if (stage_on && W > 0 && K * W * 4 <= 0x7fffffff) {
-      const size_t bytes = sizeof(float) * (size_t)((d + W - 1) / W) * (size_t)(K * W);
-      if (bytes > c->stage_bytes) {
-        if (c->stage) HIPCHK(hipFree(c->stage));   // (hipFree waits for queued work)
-        c->stage = nullptr;
-        c->stage_bytes = 0;
-        if (hipMalloc(&c->stage, bytes) == hipSuccess) c->stage_bytes = bytes;
-        else { (void)hipGetLastError(); c->stage = nullptr; }
-      }
-      if (c->stage) {
+    if (stage_enabled() && W > 0 && K * W * 4 <= 0x7fffffff) {
+      if (ensure_stage(c, sizeof(float) * (size_t)((d + W - 1) / W) * (size_t)(K * W))) {
         HIPCHK(launch_rows_to_panels(X, K, d, ldx, c->stage, W, K * W, s));
         gm_opts o2 = *o;
         o2.layout = GM_LAYOUT_PANELS;
@@ -980,25 +993,13 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
   HIPCHK(order.err);
   // Row-major AirComp problems over >= 64 passes: pack them once into the context's panel
   // buffer and stream every pass from it, as gm_weiszfeld_f32 does (C5 AirComp reading on
-  // rows: every problem runs all 1000 iterations).  GMAGG_STAGE_PANELS=0: off.
+  // rows: every problem runs all 1000 iterations).
   if (!panels && o->mode == GM_MODE_AIRCOMP && o->maxiter >= 64 &&
       P * K * d >= ((int64_t)1 << 24)) {
-    static const bool stage_on = [] {
-      const char* e = getenv("GMAGG_STAGE_PANELS");
-      return !(e && atoi(e) == 0);
-    }();
     const int64_t W = gm_panel_width(K);
-    if (stage_on && W > 0 && K * W * 4 <= 0x7fffffff) {
+    if (stage_enabled() && W > 0 && K * W * 4 <= 0x7fffffff) {
       const int64_t pst = (d + W - 1) / W * K * W;   // problem stride (floats)
-      const size_t bytes = sizeof(float) * (size_t)(P * pst);
-      if (bytes > c->stage_bytes) {
-        if (c->stage) HIPCHK(hipFree(c->stage));   // (hipFree waits for queued work)
-        c->stage = nullptr;
-        c->stage_bytes = 0;
-        if (hipMalloc(&c->stage, bytes) == hipSuccess) c->stage_bytes = bytes;
-        else { (void)hipGetLastError(); c->stage = nullptr; }
-      }
-      if (c->stage) {
+      if (ensure_stage(c, sizeof(float) * (size_t)(P * pst))) {
         for (int64_t p = 0; p < P; ++p)
           HIPCHK(launch_rows_to_panels(X + p * ldp, K, d, ldx, c->stage + p * pst, W, K * W, s));
         gm_opts o2 = *o;

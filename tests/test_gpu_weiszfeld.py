@@ -190,17 +190,19 @@ def test_gm_philox_reproducible_and_close_to_ideal():
     assert rel_l2(a.cpu().numpy(), ideal.cpu().numpy()) < 0.05
 
 
-@pytest.mark.parametrize("K,d,exact", [(300, 1 << 20, True), (50, 1 << 22, False),
-                                         (1000, 65537, False)])
-def test_gm_rows_staged_as_panels(K, d, exact):
+@pytest.mark.parametrize("K,d,pad,exact", [(300, 1 << 20, 0, True), (300, 1 << 20, 4, True),
+                                             (50, 1 << 22, 0, False), (1000, 65537, 0, False)])
+def test_gm_rows_staged_as_panels(K, d, pad, exact):
     """Row-major AirComp gm with >= 64 passes on K*d >= 2^24 packs a panel copy once and
     streams every pass from it (api.hip gm_weiszfeld_f32).  Against the row-major passes
     (algo="stream"): bit-identical where both run the same tile (K=300, d % 4 == 0),
     relative L2 1e-5 otherwise (K=50: another tile; d odd: float1 rows); the same
-    iteration count (gm runs to maxiter).  Sizes beyond the register-resident kernel."""
+    iteration count (gm runs to maxiter).  Sizes beyond the register-resident kernel;
+    pad > 0: strided rows (ldx = d + pad)."""
     g = torch.Generator().manual_seed(K + d)
-    X = (0.05 * torch.randn(K, d, generator=g)).cuda()
+    X = (0.05 * torch.randn(K, d + pad, generator=g)).cuda()[:, :d]
     X[: K // 10] += 0.3
+    assert X.stride(0) == d + pad
     g0 = (0.01 * torch.randn(d, generator=g)).cuda()
     o = {"maxiter": 64, "tol": 1e-5, "noise_var": 1e-2, "P_max": 1, "seed": 99, "guess": g0}
     a = bz().gm(X, o)
