@@ -715,9 +715,10 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   // so the copy pays for itself after ~35 passes.  Results equal the row-major passes' bit
   // for bit where both run the same tile (K outside 32 < K <= 64 and 128 < K <= 256, V = 4).
   // If the buffer cannot be allocated the rows are streamed (ensure_stage).
-  if (!panels && algo == GM_ALGO_AUTO && !sharded && !c->comm && !c->ar_fn &&
-      o->mode == GM_MODE_AIRCOMP && o->has_noise && !host_noise_req && o->maxiter >= 64 &&
-      K * d >= ((int64_t)1 << 24)) {
+  // d-sharded calls too: the layout changes no collective (one all-reduce per pass either
+  // way), so a rank may decide it from its own shard.
+  if (!panels && algo == GM_ALGO_AUTO && o->mode == GM_MODE_AIRCOMP && o->has_noise &&
+      !host_noise_req && o->maxiter >= 64 && K * d >= ((int64_t)1 << 24)) {
     const int64_t W = gm_panel_width(K);
     if (stage_enabled() && W > 0 && K * W * 4 <= 0x7fffffff) {
       if (ensure_stage(c, sizeof(float) * (size_t)((d + W - 1) / W) * (size_t)(K * W))) {

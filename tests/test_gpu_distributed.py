@@ -136,6 +136,27 @@ def test_sharded_gm_philox_world1(world1, transport, layout):
     assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-6
 
 
+@pytest.mark.parametrize("transport", ["rccl", "torch"])
+def test_sharded_gm_rows_staged_world1(world1, transport):
+    """Sharded AirComp gm on rows over >= 64 passes on a large shard streams from the
+    context's panel copy (api.hip): the same result as the unsharded row-major passes."""
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd.sharded import ShardedGM
+    K, d = 300, 65_536
+    X, g0 = _fill(K, d, 60, seed=78)
+    opts = {"maxiter": 64, "tol": 1e-5, "guess": g0, "noise_var": 1e-2, "seed": 4243}
+    want = bz.gm(X, dict(opts, algo="stream"))
+    sg = ShardedGM(d, transport=transport)
+    try:
+        got = sg.gm(X, dict(opts))
+        torch.cuda.synchronize()
+        res = sg.last_result
+    finally:
+        sg.close()
+    assert (res.iters, res.algo) == (64, "stream")
+    assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-6
+
+
 def test_sharded_requires_guess_and_seed(world1):
     from byzantine_aircomp_amd.sharded import ShardedGM
     sg = ShardedGM(1024, transport="torch")
