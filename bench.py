@@ -215,19 +215,30 @@ def cpu_baseline(X, g0, agg, var, iters, d_full, budget, max_cols):
                        + ("" if dc == d_full else ", linear in d (extrapolated)"))}
 
 
-def run_c5(args, json_out):
+def run_c5(args, json_out, rank=0, world=1):
     """BASELINE config C5: a draw.ipynb-style Monte-Carlo sweep of `args.problems`
     independent K=50 x d=100k aggregations over var in {0, 1e-3, 1e-2, 1e-1} x
     B in {0, 5, 10}.  One step = the whole sweep: per var group (problems/4 each,
     in batches of <= 1024) one batched call, and for var > 0 in the `prenoise`
     reading (the reference's `--agg gm2 --var v`, M:351-353) the batched OMA
     pre-noise (M:385-394) first — both inside the timed region.  Inputs are
-    regenerated on the device (untimed) before every step, since OMA is in place."""
+    regenerated on the device (untimed) before every step, since OMA is in place.
+
+    N > 1 (problems sharded over GPUs): every rank runs its own sweep of
+    `args.problems` problems (seeds offset by rank; no collective on the data path, a
+    gloo barrier and max-over-ranks timing around each step): weak scaling, value = all
+    ranks' problems / the slowest rank's time."""
     import byzantine_aircomp_amd as bz
     from byzantine_aircomp_amd import _lib
     from byzantine_aircomp_amd.batched import gm2_batched, gm_batched, oma_batched
-    dev = torch.device("cuda", 0)
+    local = 0 if args.one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    rs = rank * 1_000_003                       # this rank's problems: other seeds
     K, d, _, _, _ = WORKLOADS["c5"]
     ctx = bz.context(dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -251,10 +262,10 @@ def run_c5(args, json_out):
             for p in range(X.shape[0]):
                 B = C5_BYZ[(c0 + p) % 3]
                 _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, X[p].data_ptr(), K, d, d, B, 0.0,
-                                                       0.05, 0.25, 0.5, 1000 * vi + c0 + p, stream),
-                           "fill")
+                                                       0.05, 0.25, 0.5, rs + 1000 * vi + c0 + p,
+                                                       stream), "fill")
             _lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), g0.numel(), 0.0, 0.01,
-                                                  777 + vi + c0, stream), "fill")
+                                                  rs + 777 + vi + c0, stream), "fill")
         for *_, X, _g, Pn in groups:
             if Pn is not None:
                 Pn.copy_rows_(X)
@@ -269,13 +280,14 @@ def run_c5(args, json_out):
             if var == 0.0:
                 _, res = gm2_batched(X, opts)
             elif reading == "prenoise" and args.separate_oma:
-                oma_batched(X, var, seed=31 + vi * 1000 + c0)
+                oma_batched(X, var, seed=rs + 31 + vi * 1000 + c0)
                 _, res = gm2_batched(X, opts)
             elif reading == "prenoise":
                 # the pre-noise fused into gm2's first pass (same draws as oma_batched)
-                _, res = gm2_batched(X, dict(opts, pre_oma_var=var, pre_oma_seed=31 + vi * 1000 + c0))
+                _, res = gm2_batched(X, dict(opts, pre_oma_var=var,
+                                             pre_oma_seed=rs + 31 + vi * 1000 + c0))
             else:
-                _, res = gm_batched(X, dict(opts, noise_var=var, seed=31 + vi * 1000 + c0))
+                _, res = gm_batched(X, dict(opts, noise_var=var, seed=rs + 31 + vi * 1000 + c0))
             torch.cuda.synchronize(dev)
             dt = time.perf_counter() - t0
             its = [r.iters for r in res]
@@ -295,10 +307,17 @@ def run_c5(args, json_out):
             fill()
             ctx.pass_timing(True)
             torch.cuda.synchronize(dev)
+            if dist is not None:
+                dist.barrier()
             t0 = time.perf_counter()
             iters, groups_out = step(reading)
             torch.cuda.synchronize(dev)
-            total += time.perf_counter() - t0
+            el = time.perf_counter() - t0
+            if dist is not None:
+                t = torch.tensor([el], dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                el = float(t[0])
+            total += el
             ms, n = ctx.pass_timing(False)
             pass_ms += ms
             launches += n
@@ -312,7 +331,7 @@ def run_c5(args, json_out):
     agg_bytes = sum(i + 1 for i in iters) * 4.0 * K * d
     alt_reading = "aircomp" if args.reading == "prenoise" else "prenoise"
     alt = None
-    if args.alt_steps != 0:
+    if args.alt_steps != 0 and world == 1:
         a_total, _, _, a_iters, a_groups = measure(alt_reading, 1, 0)
         alt = {"reading": alt_reading, "value": len(a_iters) / a_total, "seconds": a_total,
                "mean_iters": sum(a_iters) / len(a_iters),
@@ -321,11 +340,11 @@ def run_c5(args, json_out):
                           for k, v in a_groups.items()}}
     traffic, traffic_src = pmc_traffic("c5", "panels" if use_panels else "rows")
     cpu = None
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:
         cpu = c5_cpu_baseline(groups[0][3][0], groups[0][4][0], mean_it, n_prob, args.cpu_budget)
     line = {
-        "metric": METRIC, "value": n_prob * args.steps / total, "unit": "aggregations/s",
-        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "metric": METRIC, "value": world * n_prob * args.steps / total, "unit": "aggregations/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": 1e3 * total / args.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (Philox on device: honest N(0,0.05^2), B rows N(0.25,0.5^2), "
@@ -338,7 +357,9 @@ def run_c5(args, json_out):
                                    "into gm2's first pass)")
                                   if args.reading == "prenoise" else " (AirComp gm for var > 0)"),
                    "K": K, "d": d, "problems": n_prob, "mean_iters": mean_it, "batch": chunk,
-                   "parallelism": "batched (one launch per pass covers every problem of a group)",
+                   "parallelism": "batched (one launch per pass covers every problem of a group)"
+                                  + (f"; problems sharded over {world} GPUs (each rank its own "
+                                     f"{n_prob}; no data-path collective)" if world > 1 else ""),
                    "layout": "panels (ProblemPanels)" if use_panels else "rows",
                    "groups": {str(k): {"problems_per_s": v["problems"] / v["seconds"],
                                        "mean_iters": v["iters"] / v["problems"]}
@@ -403,9 +424,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if args.workload == "c5":
-        if world != 1:
-            raise SystemExit("c5 is a one-GPU batched sweep (problems are independent)")
-        return run_c5(args, json_out)
+        if world != args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+        run_c5(args, json_out if rank == 0 else open(os.devnull, "w"), rank, world)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
     local = 0 if args.one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
