@@ -25,7 +25,8 @@
 // it has read every block's pass p+1, which each block published after reading
 // pass p, so no pass is overwritten before every block has read it.
 // The iterate never leaves the chip until the final write.  Draw keys are the
-// same as the launch-per-phase path's, so both give the same gm results.
+// same as the launch-per-phase path's, so both give the same gm results to rounding
+// (the K <= 64 AirComp coefficients are formed in fp32 here, in fp64 there).
 #include "device_util.h"
 #include "gmagg_internal.h"
 #include "philox.h"
@@ -350,7 +351,6 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         } else {
           const float s = sqrtf((float)(s_wp[1] / (double)d));      // M:146
           const float thr = (s * s) * 500.0f;                         // M:152
-          const double s2 = (double)s * (double)s;
           double ck = 0.0;
           if (kv) {
             float h2;
@@ -362,11 +362,13 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
               const float hr = n4[0] * 0.70710678118654752f, hi = n4[1] * 0.70710678118654752f;
               h2 = hr * hr + hi * hi;                                 // M:403
             }
+            // fp32, the reference's own precision (M:403-407): the wave's fp64 divisions
+            // and square roots sat on the iteration's critical path; C2 6.38 -> 6.24-6.35 ms
+            // per aggregation (profiles/r2_c2_kspace_fp32.txt)
             const float dist = clamp_dist(s_d2[k], a.eps);
-            const double dd = (double)dist;
-            const double pk = (s_r[k] + s2) / (dd * dd * (double)(d + 1)) / (double)h2;   // M:404
-            const double pup = pk != pk ? pk : fmax(pk, (double)thr);  // M:405
-            ck = sqrt(a.P_max / pup) / dd;                            // M:407
+            const float pk = ((float)s_r[k] + s * s) / (dist * dist * (float)(d + 1)) / h2;   // M:404
+            const float pup = pk != pk ? pk : fmaxf(pk, thr);          // M:405
+            ck = (double)(sqrtf((float)a.P_max / pup) / dist);         // M:407
           }
           const double Sc = wave_sum(ck);
           const double nd = !a.has_noise ? 0.0
