@@ -35,6 +35,7 @@ There is no CPU path: without a GPU or without libgmagg.so these raise.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import math
 import os
@@ -133,6 +134,20 @@ class Context:
 _contexts: dict[int, Context] = {}
 
 
+def close_all():
+    """Destroy every per-device context now (workspace, pinned host buffer, events).
+    Registered with atexit, so it runs in Py_Finalize — before the C-level exit
+    handlers that tear the HIP runtime down — instead of from Context.__del__ during
+    interpreter teardown, when the runtime (or a profiler intercepting it) may already
+    be finalised."""
+    for ctx in list(_contexts.values()):
+        ctx.close()
+
+
+if os.environ.get("GMAGG_ATEXIT_CLOSE", "1") != "0":    # (=0: the round-2 behaviour, A/B)
+    atexit.register(close_all)
+
+
 def context(device: torch.device | int | None = None) -> Context:
     if not torch.cuda.is_available():
         raise RuntimeError("byzantine_aircomp_amd needs a ROCm GPU (torch.cuda.is_available() "
@@ -214,7 +229,9 @@ def _weiszfeld(wList: torch.Tensor, options: dict, aircomp: bool):
     # keys the Philox draws as OMA(..., seed=)).  With the default guess (the column mean
     # of the NOISY rows) it runs as the separate OMA first.
     pre_var = None if aircomp else opts.get("pre_oma_var")
-    pre_seed = _seed({"seed": opts.get("pre_oma_seed")}) if pre_var is not None else 0
+    # (the Philox key is drawn only where Philox draws are made: with host draws OMA
+    # replays the reference's torch.normal sequence, which an extra randint would shift)
+    pre_seed = opts.get("pre_oma_seed")
     if pre_var is not None and (opts.get("guess") is None or wList.device.type != "cuda"
                                 or _noise_source(opts) == _lib.GM_NOISE_HOST):
         # (the reference's own draws are host-side: OMA replays them itself)
@@ -256,7 +273,7 @@ def _weiszfeld(wList: torch.Tensor, options: dict, aircomp: bool):
     if pre_var is not None:
         o.pre_oma = 1
         o.pre_oma_var = float(pre_var)
-        o.pre_oma_seed = pre_seed
+        o.pre_oma_seed = _seed({"seed": pre_seed})
     cb = None
     if aircomp:
         var = opts["noise_var"]
@@ -276,6 +293,10 @@ def _weiszfeld(wList: torch.Tensor, options: dict, aircomp: bool):
                                             out.data_ptr(), C.byref(o), C.byref(res),
                                             _stream_ptr(X.device)), "gm_weiszfeld_f32")
     last_result = _result(res)
+    if pre_var is not None and not isinstance(wList, ClientPanels) and X is not wList:
+        # a strided view was packed into a copy: the fused pre-noise landed in the
+        # copy, and OMA's contract is in place on wList (M:351-352, as OMA() copies back)
+        wList.copy_(X)
     return out if wList.device == out.device else out.to(wList.device)
 
 

@@ -82,6 +82,7 @@ class ProblemPanels:
 
 
 def _run(X, options: dict, aircomp: bool):
+    X_in = X
     panels = isinstance(X, ProblemPanels)
     if panels:
         P, K, d = X.shape
@@ -135,6 +136,8 @@ def _run(X, options: dict, aircomp: bool):
         _lib.check(ctx.lib.gm_weiszfeld_batched_f32(
             ctx.handle, buf.data_ptr(), P, K, d, ldx, ldp, g0.data_ptr(), d,
             out.data_ptr(), d, C.byref(o), res, _stream_ptr(X.device)), "gm_weiszfeld_batched_f32")
+    if pre_var is not None and X is not X_in:
+        X_in.copy_(X)          # the fused pre-noise is in place on the caller's problems
     results = [GMResult(r.iters, r.last_movement, bool(r.converged),
                         _ALGO_NAMES.get(r.algo_used, "?")) for r in res]
     return out, results

@@ -14,10 +14,12 @@
 //      wave, lane = client, when K <= 64,
 //   3. runs phases A/B of the streaming pass on its register tiles,
 //   4. publishes its partials.
-// The exchange is the data itself: every partial is an fp64 value carried by two
-// 8-byte {tag, 32-bit half} granules, each written by ONE agent-scope relaxed
+// The exchange is the data itself: every per-block partial (D2_k, ||x_k||^2, the
+// movement and ||g||^2) is the block's fp64 sum rounded once to fp32 and carried by
+// ONE 8-byte {tag, fp32 value} granule written by one agent-scope relaxed
 // (write-through) store; readers poll the granules with agent-scope relaxed loads
-// until every tag equals the pass (cdna_hip_programming.md Guideline 16, R2).  No
+// until every tag equals the pass (cdna_hip_programming.md Guideline 16, R2), and
+// sum the blocks' values in fp64 in a fixed order.  No
 // grid barrier, no release/acquire fences: the r1 version (62 one-chunk blocks,
 // counter barrier + fenced slab) spent 5.05 us of a 12.4 us iteration in the
 // barrier and 2.15 us in the slab reduction.  Passes alternate
@@ -25,8 +27,9 @@
 // it has read every block's pass p+1, which each block published after reading
 // pass p, so no pass is overwritten before every block has read it.
 // The iterate never leaves the chip until the final write.  Draw keys are the
-// same as the launch-per-phase path's, so both give the same gm results to rounding
-// (the K <= 64 AirComp coefficients are formed in fp32 here, in fp64 there).
+// same as the launch-per-phase path's, so both give the same gm results to rounding:
+// the two differ by the per-block fp32 rounding of the partials above and, at K <= 64,
+// by the AirComp coefficients formed in fp32 here (fp64 there).
 #include "device_util.h"
 #include "gmagg_internal.h"
 #include "philox.h"
@@ -306,26 +309,45 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         if (lane == 0)
           s_nd = a.has_noise ? normal1(a.seed, kStreamNoise, (uint64_t)it, (uint64_t)d) : 0.f;
       }
-      bool ok = true;
-      for (int t = tid; t < G * ncol; t += blockDim.x) {
-        const int g = t / ncol, cc = t - g * ncol;
-        const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
-        double sum;
-        if (!gather_value(in + v, NV, (unsigned)g, (unsigned)G, nb, tag, tmo, sum)) {
-          ok = false;
-          break;
-        }
-        s_part[t] = sum;
-      }
-      if (!ok) s_ok = 0;
-      __syncthreads();
-      if (s_ok == 0) return;                       // timed out: every thread leaves
-      for (int cc = tid; cc < ncol; cc += blockDim.x) {
-        double sum = 0.0;
-        for (int g = 0; g < G; ++g) sum += s_part[g * ncol + cc];
+      // G > 1 only when G * ncol <= blockDim (= NW * 64 = the size of s_part): one
+      // (group, value) per thread.  G == 1 (ncol > blockDim / 2, e.g. INIT's 2K + 2
+      // values at K >= 512) sums every block in one thread and stores the value
+      // directly: s_part is not used, so no value count can overrun it.
+      auto store_value = [&](int cc, double sum) {
         if (cc < K) s_d2[cc] = sum;
         else if (cc < nk) s_r[cc - K] = sum;
         else s_wp[cc - nk] = sum;
+      };
+      bool ok = true;
+      if (G == 1) {
+        for (int cc = tid; cc < ncol; cc += blockDim.x) {
+          const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
+          double sum;
+          if (!gather_value(in + v, NV, 0u, 1u, nb, tag, tmo, sum)) {
+            ok = false;
+            break;
+          }
+          store_value(cc, sum);
+        }
+        if (!ok) s_ok = 0;
+        __syncthreads();
+        if (s_ok == 0) return;                     // timed out: every thread leaves
+      } else {
+        if (tid < G * ncol) {
+          const int g = tid / ncol, cc = tid - g * ncol;
+          const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
+          double sum;
+          if (gather_value(in + v, NV, (unsigned)g, (unsigned)G, nb, tag, tmo, sum)) s_part[tid] = sum;
+          else ok = false;
+        }
+        if (!ok) s_ok = 0;
+        __syncthreads();
+        if (s_ok == 0) return;                     // timed out: every thread leaves
+        for (int cc = tid; cc < ncol; cc += blockDim.x) {
+          double sum = 0.0;
+          for (int g = 0; g < G; ++g) sum += s_part[g * ncol + cc];
+          store_value(cc, sum);
+        }
       }
       __syncthreads();   // (s_wp is read in place: its next write follows this iteration's barriers)
     }

@@ -69,6 +69,14 @@ def torch_allreduce_adapter(group=None, device: torch.device | None = None):
     return fn
 
 
+def _aligned(shards, d_total: int) -> bool:
+    """Every rank's shard lies in [0, d_total), 256-aligned at lo and 4-aligned at hi
+    (so d_total % 4 == 0 gives every rank the float4 rows the Gram path needs).  Tiling
+    is not required: a one-GPU rehearsal runs rank r's shard of a larger job alone."""
+    return all(0 <= lo <= hi <= d_total and lo % ALIGN == 0 and (hi % 4 == 0 or hi == d_total)
+               for lo, hi in shards)
+
+
 class ShardedGM:
     """gm2 / gm on this rank's column shard of a d_total-long update."""
 
@@ -88,9 +96,14 @@ class ShardedGM:
             self.lo, self.hi = shard_range(d_total, self.world, self.rank)
         else:
             self.lo, self.hi = int(shard[0]), int(shard[1])
-            if not (0 <= self.lo <= self.hi <= d_total) or self.lo % ALIGN:
-                raise ValueError(f"shard {shard} of d_total={d_total}: need 0 <= lo <= hi <= "
-                                 f"d_total and lo % {ALIGN} == 0")
+            # validated collectively: a shard that only one rank rejects (or that only one
+            # rank's library call would refuse inside a collective sequence) hangs the rest
+            shards = [None] * self.world
+            dist.all_gather_object(shards, (self.lo, self.hi), group=group)
+            if not _aligned(shards, d_total):
+                raise ValueError(f"shards {shards} of d_total={d_total}: each must be [lo, hi) "
+                                 f"within [0, d_total) with lo % {ALIGN} == 0 and hi % 4 == 0 "
+                                 "(or hi == d_total)")
         self.ctx = Context(self.device.index)
         self.ctx.set_shard(d_total, self.lo)
         if transport == "rccl":
@@ -117,11 +130,14 @@ class ShardedGM:
         opts.update(options or {})
         if X.shape[1] != self.d_local or X.device != self.device or X.dtype != torch.float32:
             raise ValueError(f"X must be fp32 [K, {self.d_local}] on {self.device}")
+        X_in = X
         if isinstance(X, ClientPanels):      # this rank's columns in the panel layout
             ptr, ldx, layout = X.data.data_ptr(), X.panel_stride, _lib.GM_LAYOUT_PANELS
         else:
-            if X.stride(1) != 1:
-                X = X.contiguous()
+            if X.stride(1) != 1 or X.data_ptr() % 16 or (X.stride(0) % 4 and X.shape[0] > 1):
+                # unit stride and float4-aligned rows, as on every other rank: the AUTO
+                # Gram decision is global, so a rank must never fall short of it locally
+                X = X.clone(memory_format=torch.contiguous_format)
             ptr, ldx, layout = X.data_ptr(), max(X.stride(0), self.d_local), _lib.GM_LAYOUT_ROWS
         K = X.shape[0]
         guess = opts.get("guess")
@@ -162,6 +178,8 @@ class ShardedGM:
                 g0.data_ptr(), out.data_ptr(), C.byref(o), C.byref(res),
                 torch.cuda.current_stream(self.device).cuda_stream), "gm_weiszfeld_f32")
         self.last_result = _result(res)
+        if o.pre_oma and X is not X_in:
+            X_in.copy_(X)      # the fused pre-noise is in place on the caller's shard
         return out
 
     def gm2(self, X, options=None):

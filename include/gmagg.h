@@ -63,15 +63,19 @@ enum gm_noise_source {
 enum gm_layout {
     GM_LAYOUT_ROWS = 0,       /* [K][ldx] row-major (the reference's torch.stack of rows) */
     GM_LAYOUT_PANELS = 1      /* [ceil(d/W)][K][W], W = gm_panel_width(K), ldx = panel stride;
-                                 streaming algorithm only (AUTO -> STREAM) */
+                                 streaming, or (gm2, K <= 256, W % 64 == 0) the guarded Gram */
 };
 
 enum gm_algo {
     GM_ALGO_AUTO = 0,
     GM_ALGO_STREAM = 1,       /* fused one-read-per-iteration streaming Weiszfeld */
     GM_ALGO_TWOPASS = 2,      /* two reads per iteration; any K */
-    GM_ALGO_GRAM = 3,         /* K x K Gram on MFMA (bf16 h+m split, 4 products), iterations in
-                                 K-space (IDEAL only, K <= 256) */
+    GM_ALGO_GRAM = 3,         /* K x K Gram on MFMA, iterations in K-space (IDEAL only, K <= 256):
+                                 scaled f16 hi/lo split, 3 v_mfma_f32_32x32x16_f16 products per
+                                 off-diagonal tile (2 on the diagonal); an f16 range overflow
+                                 reruns the bf16 h+m split (4 products, rows) or the streaming
+                                 path (panels); the result is kept only if the a-posteriori
+                                 guard passes (gm_result.guard / gram_kind) */
     GM_ALGO_RESIDENT = 4,     /* small problems: X held in VGPRs, all iterations in one launch */
     GM_ALGO_GRAM_F32 = 5      /* the Gram on the exact f32-input MFMA (4x the issue cycles) */
 };
@@ -180,9 +184,10 @@ int gm_weiszfeld_batched_f32(gm_ctx* ctx, const float* X, int64_t P, int64_t K, 
 
 /* The reference's other aggregators (MNIST_Air_weight.py:186-204), out[d]:
  *   gm_mean_f32          mean(wList, options)          M:186-187
- *   gm_median_f32        median(wList, options)        M:194-195 (lower median), K <= 256
- *   gm_trimmed_mean_f32  trimmed_mean(wList, options)  M:189-192, trim = int(0.1 K) per end, K <= 256
- *   gm_krum_f32          Krum(wList, options)          M:197-204, K <= 1024; *index = chosen row */
+ *   gm_median_f32        median(wList, options)        M:194-195 (lower median), K <= 2048
+ *   gm_trimmed_mean_f32  trimmed_mean(wList, options)  M:189-192, trim = int(0.1 K) per end, K <= 2048
+ *   gm_krum_f32          Krum(wList, options)          M:197-204, K <= 4096; *index = chosen row
+ * Larger K returns GM_ERR_UNSUPPORTED. */
 int gm_mean_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t ldx, float* out,
                 void* stream);
 int gm_median_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t ldx, float* out,

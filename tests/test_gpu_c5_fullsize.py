@@ -1,0 +1,138 @@
+"""BASELINE C5 at its configured size: K=50 x d=100,000 problems in large batches.
+
+The bench's C5 sweep (bench.py run_c5) runs 1024-problem ProblemPanels batches
+through the batched kernels; these tests pin that exact shape against the oracle
+on a sample of problems (first, last and interior ones of the batch), so the
+sweep's aggregates are compared with the reference's algorithm at full size:
+
+  * the `--agg gm2 --var v` reading (OMA pre-noise, then gm2: M:351-353 ->
+    M:385-394, M:162-184) with the pre-noise fused into gm2's first pass, the
+    noisy problems copied back and checked with oracle.gm2 (north_star: rel L2
+    <= 1e-5, iterations +-1);
+  * the AirComp reading (gm, M:131-160 + OMA2 M:396-414) with Philox draws:
+    problem p keyed seed + p * SEED_STRIDE, checked with oracle.gm fed
+    oracle/philox.gm_draws(seed_p) (the same iteration count; rel L2 <= 1e-5, or at
+    least as close to the fp64 result as the reference's own fp32: see the test).
+
+Data: the bench's own device recipe (gm_fill_clients_f32: honest rows
+N(0, 0.05^2), the last B rows N(0.25, 0.5^2), B in {0, 5, 10} by problem;
+guess N(0, 0.01^2)).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_l2
+from oracle import aggregators as orc
+
+pytestmark = pytest.mark.gpu
+
+K, D = 50, 100_000
+BYZ = (0, 5, 10)
+
+
+def _fill(P, seed):
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd import _lib
+    ctx = bz.context()
+    s = torch.cuda.current_stream().cuda_stream
+    X = torch.empty(P, K, D, device="cuda")
+    for p in range(P):
+        _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, X[p].data_ptr(), K, D, D, BYZ[p % 3],
+                                               0.0, 0.05, 0.25, 0.5, seed + p, s), "fill")
+    g0 = torch.empty(P, D, device="cuda")
+    _lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), g0.numel(), 0.0, 0.01,
+                                          seed + 777, s), "fill")
+    return X, g0
+
+
+def _problem_rows(Pn, p):
+    """Problem p of a ProblemPanels batch as its [K, d] row-major matrix (host)."""
+    full = Pn.data[p].permute(1, 0, 2).reshape(Pn.K, Pn.npan * Pn.W)
+    return full[:, :Pn.d].cpu()
+
+
+def _sample(P):
+    return sorted({0, 1, 2, P // 3, P // 2, P - 3, P - 2, P - 1})
+
+
+@pytest.mark.parametrize("var", [1e-3, 1e-1])
+def test_c5_prenoise_gm2_full_batch(var):
+    """1024 problems of K=50 x d=100k in ProblemPanels, `--agg gm2 --var v`: the OMA
+    pre-noise fused into the INIT pass, then gm2 per problem to its own tol test.
+    Each sampled problem's noisy matrix (read back from the panels) through oracle.gm2
+    from the same guess: rel L2 <= 1e-5 and iterations +-1 (north_star)."""
+    from byzantine_aircomp_amd.batched import ProblemPanels, gm2_batched
+    P = 1024
+    X, g0 = _fill(P, seed=5000)
+    Pn = ProblemPanels.from_rows(X)
+    del X
+    out, res = gm2_batched(Pn, {"maxiter": 1000, "tol": 1e-5, "guess": g0,
+                                "pre_oma_var": var, "pre_oma_seed": 77})
+    torch.cuda.synchronize()
+    assert all(r.converged for r in res)
+    for p in _sample(P):
+        Xp = _problem_rows(Pn, p)
+        want, tr = orc.gm2(Xp.clone(), {"maxiter": 1000, "tol": 1e-5, "guess": g0[p].cpu()})
+        err = rel_l2(out[p].cpu().numpy(), want.numpy())
+        assert err <= 1e-5, (p, err)
+        assert abs(res[p].iters - tr.iters) <= 1, (p, res[p].iters, tr.iters)
+
+
+def test_c5_prenoise_noise_is_oma():
+    """The pre-noise the full batch received is the batched OMA's draws (problem p keyed
+    pre_oma_seed + p * SEED_STRIDE), checked on sampled problems against the Philox
+    restatement of OMA (oracle/philox.oma_philox)."""
+    from byzantine_aircomp_amd.batched import SEED_STRIDE, ProblemPanels, gm2_batched
+    from oracle.philox import oma_philox
+    P, var, seed = 256, 1e-2, 91
+    X, g0 = _fill(P, seed=6000)
+    Pn = ProblemPanels.from_rows(X)
+    gm2_batched(Pn, {"maxiter": 1000, "tol": 1e-5, "guess": g0, "pre_oma_var": var,
+                     "pre_oma_seed": seed})
+    torch.cuda.synchronize()
+    for p in (0, 1, P // 2, P - 1):
+        want = oma_philox(X[p].cpu().numpy(), var, (seed + p * SEED_STRIDE) % 2 ** 64)
+        got = _problem_rows(Pn, p).numpy().astype(np.float64)
+        err = np.abs(got - want) / (1.0 + np.abs(want))
+        assert err.max() <= 2e-6, (p, err.max())
+
+
+@pytest.mark.parametrize("var", [1e-2, None])
+def test_c5_aircomp_gm_full_batch(var):
+    """256 problems of K=50 x d=100k in ProblemPanels through the AirComp gm with Philox
+    draws (10 iterations: gm never meets tol, and the oracle's CPU cost is per
+    iteration); sampled problems vs oracle.gm fed the same draws.
+
+    Bar: rel L2 <= 1e-5 against the fp32 oracle, OR at least as close to the same
+    iteration in fp64 (the oracle run on float64 X / guess with the same draws) as the
+    reference's own fp32 arithmetic is.  On this recipe gm's fp32 result drifts from fp64
+    by 4e-6 .. 6e-5 within 5-10 iterations (measured on CPU: B=5 at 5 iterations
+    2.3e-5, B=10 at 10 iterations 5.2e-5), far above a mere summation-order change
+    (row permutation: 1e-9 .. 2e-6), and the kernels' K-space step runs in fp64 (the
+    reference's OMA2 is fp32), so the kernel lands between the two; 1e-5 against fp32
+    alone would test which rounding the reference happens to make, not correctness."""
+    from byzantine_aircomp_amd.batched import SEED_STRIDE, ProblemPanels, gm_batched
+    from oracle.philox import gm_draws
+    P, it, seed = 256, 10, 4242
+    X, g0 = _fill(P, seed=7000)
+    Pn = ProblemPanels.from_rows(X)
+    out, res = gm_batched(Pn, {"maxiter": it, "tol": 1e-5, "guess": g0, "noise_var": var,
+                               "seed": seed})
+    torch.cuda.synchronize()
+    assert [r.iters for r in res] == [it] * P
+    for p in (0, 1, 2, P // 2, P - 2, P - 1):
+        runs = []
+        for dt in (torch.float32, torch.float64):
+            draw = gm_draws((seed + p * SEED_STRIDE) % 2 ** 64, D)
+            if var is None:
+                draw.no_noise()
+            ref, tr = orc.gm(X[p].cpu().to(dt), {"maxiter": it, "tol": 1e-5, "noise_var": var,
+                                                 "P_max": 1, "guess": g0[p].cpu().to(dt)},
+                             draw=draw)
+            assert tr.iters == it
+            runs.append(ref.numpy())
+        want32, want64 = runs
+        got = out[p].cpu().numpy()
+        err32, err64, ref_err = rel_l2(got, want32), rel_l2(got, want64), rel_l2(want32, want64)
+        assert err32 <= 1e-5 or err64 <= ref_err, (p, err32, err64, ref_err)

@@ -229,7 +229,7 @@ def test_gm2_shapes_vs_oracle(K, d):
     want, tr = orc.gm2(X.clone(), dict(opts))
     got = bz().gm2(X.cuda(), dict(opts, guess=p.cuda()))
     assert rel_l2(got.cpu().numpy(), want.numpy()) <= TOL
-    assert abs(bz().aggregators.last_result.iters - tr.iters) <= max(ITER_SLACK, tr.iters // 10)
+    assert abs(bz().aggregators.last_result.iters - tr.iters) <= ITER_SLACK
 
 
 def test_gm2_strided_rows():
@@ -334,7 +334,7 @@ def test_gram_shapes_vs_oracle(K, d, algo):
     got = bz().gm2(X.cuda(), dict(opts, guess=p.cuda(), algo=algo))
     assert bz().aggregators.last_result.algo == algo
     assert rel_l2(got.cpu().numpy(), want.numpy()) <= TOL
-    assert abs(bz().aggregators.last_result.iters - tr.iters) <= max(ITER_SLACK, tr.iters // 10)
+    assert abs(bz().aggregators.last_result.iters - tr.iters) <= ITER_SLACK
 
 
 def test_gram_matches_stream_at_c4_scale():
@@ -517,3 +517,60 @@ def test_batched_pre_oma_equals_oma_then_gm2(layout, d):
     assert torch.equal(da, db)
     assert torch.equal(a, b)
     assert [r.iters for r in ra] == [r.iters for r in rb]
+
+
+def test_pre_oma_strided_view_is_noised_in_place():
+    """A strided [K, d] view (ldx = d + 3, unaligned for float4) is packed into a copy for
+    the kernels; the fused pre-noise must still land in the caller's tensor, as OMA()
+    does (M:351-352 mutates weight_f in place).  Single, batched and sharded calls."""
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd.batched import gm2_batched, oma_batched
+    K, d = 300, 4096
+    g = torch.Generator().manual_seed(12)
+    base = (0.05 * torch.randn(K, d + 3, generator=g)).cuda()
+    g0 = (0.01 * torch.randn(d, generator=g)).cuda()
+    opts = {"maxiter": 30, "tol": 1e-5, "guess": g0}
+    ref = base[:, :d].clone()
+    bz.OMA(ref, 1e-2, seed=5)
+    want = bz.gm2(ref, dict(opts))
+    big = base.clone()
+    view = big[:, :d]
+    assert not view.is_contiguous()
+    got = bz.gm2(view, dict(opts, pre_oma_var=1e-2, pre_oma_seed=5))
+    assert torch.equal(view, ref)
+    assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-6
+    # batched: a [P, K, d] view with padded rows
+    P = 3
+    bb = (0.05 * torch.randn(P, 50, d + 4, generator=g)).cuda()
+    gb = (0.01 * torch.randn(P, d, generator=g)).cuda()
+    vref = bb[:, :, :d].clone()
+    oma_batched(vref, 1e-2, seed=9)
+    vb = bb[:, :, :d]
+    vb = vb.transpose(0, 1).contiguous().transpose(0, 1)     # non-standard problem stride
+    gm2_batched(vb, {"maxiter": 30, "tol": 1e-5, "guess": gb, "pre_oma_var": 1e-2,
+                     "pre_oma_seed": 9})
+    assert torch.equal(vb, vref)
+
+
+def test_pre_oma_host_draws_keep_reference_sequence():
+    """With noise_source='host' the pre-noise replays the reference's torch.normal draws
+    (M:389-392); the call must not consume any other draw from the CPU generator first,
+    so OMA + gm2 here equals the oracle's OMA then gm2 from the same generator state."""
+    import byzantine_aircomp_amd as bz
+    K, d = 20, 1000
+    g = torch.Generator().manual_seed(3)
+    X = 0.05 * torch.randn(K, d, generator=g)
+    p = 0.01 * torch.randn(d, generator=g)
+    torch.manual_seed(4321)
+    Xr = X.clone()
+    orc.oma_(Xr, 1e-2)
+    want, _ = orc.gm2(Xr, {"maxiter": 100, "tol": 1e-5, "guess": p.clone()})
+    after_ref = torch.randint(0, 2 ** 30, (1,)).item()
+    torch.manual_seed(4321)
+    Xg = X.clone().cuda()
+    got = bz.gm2(Xg, {"maxiter": 100, "tol": 1e-5, "guess": p.cuda(), "pre_oma_var": 1e-2,
+                      "noise_source": "host"})
+    after_gpu = torch.randint(0, 2 ** 30, (1,)).item()
+    assert after_ref == after_gpu              # the same number of CPU-generator draws
+    assert torch.equal(Xg.cpu(), Xr)
+    assert rel_l2(got.cpu().numpy(), want.numpy()) <= TOL
