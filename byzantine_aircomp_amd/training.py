@@ -118,9 +118,30 @@ def dataflip(messages, byzantinesize):
 
 
 def weightflip(messages, byzantinesize):
-    """M:380-383, on the device matrix."""
+    """M:380-383, on the device matrix: the last B rows become -w - 2 * sum(honest) / B.
+    On ClientPanels ([npan][K][W]) the same per-column rewrite, panel by panel: the
+    honest sum runs over each panel's first K - B rows (the padding columns >= d hold 0
+    in every row, so they stay 0)."""
+    from .panels import ClientPanels
+    if isinstance(messages, ClientPanels):
+        D = messages.data
+        honest_sum = D[:, :-byzantinesize, :].sum(dim=1, keepdim=True)
+        D[:, -byzantinesize:, :].mul_(-1).add_(honest_sum / byzantinesize, alpha=-2)
+        return
     honest_sum = messages[:-byzantinesize].sum(dim=0)
     messages[-byzantinesize:].mul_(-1).add_(honest_sum / byzantinesize, alpha=-2)
+
+
+def _oma_host(message, noise_var):
+    """OMA (M:385-394) on a CPU matrix, with the reference's own torch expression and
+    draw order (the device paths are aggregators.OMA / the fused gm2 pre-noise)."""
+    K, d = message.shape
+    sd = noise_var ** 0.5
+    h_re = torch.normal(torch.zeros(K, 1), 2 ** -0.5)
+    h_im = torch.normal(torch.zeros(K, 1), 2 ** -0.5)
+    n_re = torch.normal(torch.zeros(K, d), sd)
+    n_im = torch.normal(torch.zeros(K, d), sd)
+    message.add_((h_re * n_re + h_im * n_im) / (h_re ** 2 + h_im ** 2))
 
 
 # ---- device-resident client packing (row f2) --------------------------------------
@@ -214,9 +235,6 @@ def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # 
         _log(f"[0/{rounds}] train: loss={tl:.4f} acc={ta:.4f} val: loss={vl:.4f} acc={va:.4f}")
 
     attack_name = attack.__name__ if attack is not None else None
-    if layout == "panels" and attack_name == "weightflip":
-        raise ValueError("layout='panels' supports the classflip / dataflip attacks (weightflip "
-                         "rewrites whole rows: use layout='rows')")
     clients = ClientUpdates(model, K, layout=layout)
     params = clients.params
     is_gm = aggregate.__name__ == "gm"
@@ -248,7 +266,9 @@ def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # 
             options = {"maxiter": 1000, "tol": 1e-5, "eta": 1, "noise_var": noise_var,
                        "guess": clients.flat(), "honestSize": honestSize}     # M:349-350
             if noise_var is not None and not is_gm:
-                if fuse_oma:
+                if X.device.type == "cpu":
+                    _oma_host(X, noise_var)               # M:351-352 on a CPU matrix
+                elif fuse_oma:
                     options["pre_oma_var"] = noise_var    # M:351-352, fused into gm2
                 else:
                     OMA(X, noise_var)                     # M:351-352

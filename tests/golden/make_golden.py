@@ -322,8 +322,50 @@ def e2e_emnist():
     print("wrote EMNIST e2e cases")
 
 
+def e2e_more():
+    """More of the reference's SGD (M:226-372) for the loop counterpart (row f4), appended
+    to golden.json (`python tests/golden/make_golden.py --e2e-more`): the weightflip and
+    dataflip attacks (M:380-383, M:324-330) under gm2, and gm2 with --var 1e-2 (the
+    reference's OMA pre-noise before a non-gm aggregator, M:351-352)."""
+    ref = load_reference()
+    torch.set_num_threads(8)
+    path = os.path.join(HERE, "golden.json")
+    manifest = json.load(open(path))
+    ce = torch.nn.CrossEntropyLoss()
+    loss = lambda o, t: ce(o, t.long())  # noqa: E731
+    xtr, ytr = synthetic_mnist(601, 2000)
+    xva, yva = synthetic_mnist(602, 500)
+    for attack, agg, var in (("weightflip", "gm2", None), ("dataflip", "gm2", None),
+                             ("classflip", "gm2", 1e-2)):
+        name = f"e2e_sgd_{attack}_{agg}" + ("" if var is None else f"_var{var:g}")
+        manifest["cases"] = [c for c in manifest["cases"] if c["name"] != name]
+        tr = torch.utils.data.TensorDataset(torch.from_numpy(xtr), torch.from_numpy(ytr))
+        va = torch.utils.data.TensorDataset(torch.from_numpy(xva), torch.from_numpy(yva))
+        model = ref.modelFactory(SEED=2021)
+        res = ref.SGD(model, gamma=1e-2, aggregate=getattr(ref, agg), weight_decay=0.0,
+                      noise_var=var, honestSize=45, byzantineSize=5,
+                      attack=getattr(ref, attack), rounds=2, displayInterval=2, SEED=2021,
+                      fixSeed=True, loss_func=loss, train_dataset=tr,
+                      validate_dataset=va, device=torch.device("cpu"), batchSize=50)
+        m, tl, ta, vl, va_, vp = res
+        w = torch.cat([p.detach().flatten() for p in m.parameters()]).numpy()
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), weights=w)
+        manifest["cases"].append({
+            "func": "SGD", "attack": attack, "aggregate": agg, "noise_var": var, "K": 50,
+            "B": 5, "rounds": 2, "displayInterval": 2, "SEED": 2021, "batchSize": 50,
+            "gamma": 1e-2, "data_seeds": [601, 602], "n_train": 2000, "n_val": 500,
+            "trainLossPath": tl, "trainAccPath": ta, "valLossPath": vl,
+            "valAccPath": va_, "variencePath": [float(v) for v in vp],
+            "name": name, "file": name + ".npz"})
+        print("wrote", name)
+    with open(path, "w") as f:
+        json.dump(manifest, f, indent=1)
+
+
 if __name__ == "__main__":
     if "--emnist" in sys.argv:
         e2e_emnist()
+    elif "--e2e-more" in sys.argv:
+        e2e_more()
     else:
         main()

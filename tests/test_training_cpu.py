@@ -108,3 +108,31 @@ def test_run_writes_reference_record(tmp_path):
                 "honestSize", "byzantineSize", "aggregate", "attack", "name"):
         assert key in saved
     assert saved["aggregate"] == "function" and len(saved["valLossPath"]) == 2
+
+
+MORE_E2E = [("weightflip", None, "e2e_sgd_weightflip_gm2"), ("dataflip", None, "e2e_sgd_dataflip_gm2"),
+            ("classflip", 1e-2, "e2e_sgd_classflip_gm2_var0.01")]
+
+
+@pytest.mark.parametrize("attack,var,name", MORE_E2E)
+def test_sgd_counterpart_bit_exact_more_attacks(attack, var, name):
+    """weightflip (M:380-383), dataflip (M:324-330) and `--agg gm2 --var 1e-2` (the OMA
+    pre-noise before a non-gm aggregator, M:351-352) through the build's loop with the
+    oracle aggregator: bit for bit with the reference's own loop."""
+    from byzantine_aircomp_amd import training as T
+    meta, arr = golden_case(name)
+    assert meta["noise_var"] == var
+    tr = torch.utils.data.TensorDataset(*synthetic_mnist(601, 2000))
+    va = torch.utils.data.TensorDataset(*synthetic_mnist(602, 500))
+    model = T.modelFactory(SEED=2021)
+    res = T.SGD(model, gamma=1e-2, aggregate=_as_aggregator("gm2"), weight_decay=0.0,
+                noise_var=var, honestSize=45, byzantineSize=5, attack=getattr(T, attack),
+                rounds=2, displayInterval=2, SEED=2021, fixSeed=True,
+                loss_func=torch.nn.CrossEntropyLoss(), train_dataset=tr, validate_dataset=va,
+                device=torch.device("cpu"), batchSize=50, verbose=False)
+    m, tl, ta, vl, vacc, vv = res
+    w = torch.cat([p.detach().flatten() for p in m.parameters()]).numpy()
+    assert np.array_equal(w, arr["weights"])
+    assert tl == meta["trainLossPath"] and vl == meta["valLossPath"]
+    assert ta == meta["trainAccPath"] and vacc == meta["valAccPath"]
+    assert [float(v) for v in vv] == meta["variencePath"]

@@ -54,7 +54,7 @@ for step in "$@"; do
       ;;
     pmc)
       name=${rest%%:*}; r2=${rest#*:}; ctr=${r2%%:*}; args=${r2#*:}; [ "$args" = "$r2" ] && args=""
-      timeout -s KILL 240 rocprofv3 --pmc "$ctr" --output-format csv -d "$out/$name" -o p -- \
+      timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d "$out/$name" -o p -- \
         python3 bench.py $args > "$out/$name.log" 2>&1 || { rc=$?; tail -20 "$out/$name.log"; exit $rc; }
       ;;
     py)
