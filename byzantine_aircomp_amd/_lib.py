@@ -93,6 +93,9 @@ SIGNATURES = [
      [_P, _P, _I64, _I64, _I64, _I64, _I64, C.c_double, C.c_uint64, _P]),
     ("gm_rows_to_panels_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _P, _I64, _I64, _P]),
     ("gm_oma_apply_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P]),
+    ("gm_client_chain_f32", C.c_int, [_P, _P, _I64, _P, _I64, _I64, _P, _I64, _I64, _I64,
+                                      C.c_int32, C.c_float, C.c_float, _P, _P, _P, _I64,
+                                      C.c_int32, _P]),
     ("gm_fill_clients_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _I64, C.c_float, C.c_float,
                                       C.c_float, C.c_float, C.c_uint64, _P]),
     ("gm_fill_normal_f32", C.c_int, [_P, _P, _I64, C.c_float, C.c_float, C.c_uint64, _P]),

@@ -1400,6 +1400,38 @@ int gm_rows_to_panels_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64
   return GM_OK;
 }
 
+int gm_client_chain_f32(gm_ctx* c, const float* data, int64_t ldd, const int64_t* labels,
+                        int64_t F, int64_t C, const int32_t* idx, int64_t K, int64_t B,
+                        int64_t honest, int32_t attack, float gamma, float weight_decay,
+                        float* W, float* b, float* X, int64_t ldx, int32_t layout, void* stream) {
+  if (!c || !data || !labels || !idx || !W || !b || !X || K < 0 || honest < 0 || ldd < F ||
+      attack < 0 || attack > 2 || (layout != GM_LAYOUT_ROWS && layout != GM_LAYOUT_PANELS))
+    return fail(GM_ERR_INVALID, "gm_client_chain_f32: bad args");
+  if (!client_chain_supported(F, C, B))
+    return fail(GM_ERR_UNSUPPORTED, "gm_client_chain_f32: needs F <= 832, C <= 64, B <= 64 "
+                "(F=%lld C=%lld B=%lld)", (long long)F, (long long)C, (long long)B);
+  const int64_t d = C * F + C;
+  ClientChainArgs a{};
+  a.data = data; a.ldd = ldd; a.labels = labels; a.F = F; a.C = C; a.idx = idx;
+  a.K = K; a.B = B; a.honest = honest; a.attack = attack; a.gamma = gamma; a.wd = weight_decay;
+  a.W = W; a.b = b; a.X = X;
+  if (layout == GM_LAYOUT_PANELS) {
+    const int64_t Wp = gm_panel_width(K);
+    if (Wp == 0 || ldx < K * Wp) return fail(GM_ERR_INVALID, "gm_client_chain_f32: panel stride");
+    int ws = 0;
+    while (((int64_t)1 << ws) < Wp) ++ws;
+    a.pstride = ldx;
+    a.wshift = ws;
+  } else {
+    if (ldx < d) return fail(GM_ERR_INVALID, "gm_client_chain_f32: ldx < C*F + C");
+    a.ldx = ldx;
+  }
+  if (K == 0) return GM_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(launch_client_chain(a, reinterpret_cast<hipStream_t>(stream)));
+  return GM_OK;
+}
+
 int gm_oma_apply_f32(gm_ctx* c, float* X, int64_t K, int64_t d, int64_t ldx, const float* hr,
                      const float* hi, const float* nr, const float* ni, void* stream) {
   if (!c || !X || !hr || !hi || !nr || !ni || K < 0 || d < 0 || ldx < d)

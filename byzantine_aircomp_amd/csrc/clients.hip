@@ -1,0 +1,207 @@
+// The K simulated clients' local SGD steps of one federated step, as ONE kernel
+// (with the aggregation on the GPU, the reference's sequential
+// client loop — K tiny forward/backward passes driven from Python, M:291-343 — is
+// what a training step costs).
+//
+// Reference semantics kept exactly (MNIST_Air_weight.py):
+//   * the model is the linear softmax classifier MLP(784, C) (M:53-61) trained with
+//     CrossEntropyLoss (mean over the batch, M:573) and plain SGD
+//     p <- p - gamma * (grad + weight_decay * p)  (M:302-303 / M:339-340);
+//   * the clients run IN SEQUENCE on one model: modelSnapshot returns the state_dict,
+//     which aliases the parameters, so "modelRecovery" restores nothing and client k
+//     starts from client k-1's updated weights (M:290, M:343) — a chain, so the K steps
+//     cannot run as independent batched gradients;
+//   * Byzantine clients (node >= honest) train on 1 - x (dataflip, M:326) or on the
+//     relabelled C-1-y (classflip, M:320; EMNIST 61-y, E:321);
+//   * client k's updated parameters become row k of the client matrix in
+//     model.parameters() order (weight [C][F] row-major, then bias [C]: flatten_list,
+//     M:206-209), written straight into the aggregator's input (rows or panels).
+// After the call W / b hold the last client's parameters, which the reference's loop
+// passes as the aggregator's guess (M:349).
+//
+// One workgroup of 512 threads (8 waves, up to 256 VGPRs each) walks the chain.  Per
+// client:
+//   A  logits z[s][c] = x_s . W_c + b_c: wave w owns samples s = w + 8 i (the batch
+//      tile stays in its registers), its lanes the features f = lane + 64 j; per group
+//      of 4 classes each lane accumulates the 8 x 4 partial dots over its features, one
+//      transpose-reduce over the wave's 64 lanes completes them (one shuffle per value
+//      instead of six);
+//   B  softmax cross-entropy gradient per sample, one wave per sample, lane = class,
+//      torch's order: log_softmax, then dz = gout - exp(logp) * sum(gout) with
+//      gout = -1/B at the label (nll_loss mean backward);
+//   C  thread = features f, f + 512: gW[c][f] = sum_s dz[s][c] x[s][f] (s ascending),
+//      the SGD update of column f of W, and the client's row of the client matrix.
+// The batch rows are gathered by index from the training set on the device (the
+// samplers' index streams are drawn on the host in the reference's order).
+#include "device_util.h"
+#include "gmagg_internal.h"
+
+namespace gmk {
+
+constexpr int kCcThreads = 512;
+constexpr int kCcWaves = kCcThreads / 64;
+constexpr int kCcSpw = 8;        // samples per wave in phase A (B <= 64)
+constexpr int kCcCg = 4;         // classes per phase-A group
+constexpr int kCcFpt = 2;        // features per thread in phase C
+constexpr int kCcNj = 13;        // features per lane in phase A: F <= 832
+constexpr int kCcCgC = 16;       // classes per phase-C group
+constexpr int kCcMaxC = 64;
+constexpr int kCcMaxB = kCcWaves * kCcSpw;
+
+__device__ __forceinline__ void put_param(const ClientChainArgs& a, int64_t k, int64_t jj, float v) {
+  if (a.pstride > 0)
+    a.X[(jj >> a.wshift) * a.pstride + k * ((int64_t)1 << a.wshift) +
+        (jj & (((int64_t)1 << a.wshift) - 1))] = v;
+  else
+    a.X[k * a.ldx + jj] = v;
+}
+
+// NJ = features per lane in phase A (F <= 64 * NJ)
+template <int NJ>
+__global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a) {
+  __shared__ float s_z[kCcMaxB][kCcMaxC + 1];     // logits, then the gradient dz (padding 0)
+  __shared__ int s_row[kCcMaxB];                  // dataset rows of the client's batch
+  __shared__ int s_lab[kCcMaxB];                  // (relabelled) targets
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int F = (int)a.F, C = (int)a.C, B = (int)a.B;
+  const float invB = 1.0f / (float)B;
+
+  for (int64_t k = 0; k < a.K; ++k) {
+    const bool byz = k >= a.honest;
+    const bool flip_x = byz && a.attack == 2;
+    if (tid < B) {
+      const int r = a.idx[k * B + tid];
+      s_row[tid] = r;
+      const int y = (int)a.labels[r];
+      s_lab[tid] = (byz && a.attack == 1) ? (C - 1 - y) : y;
+    }
+    __syncthreads();
+
+    // ---- A: logits.  The wave's batch tile: samples w + 8 i, features lane + 64 j
+    float xr[kCcSpw][NJ];
+#pragma unroll
+    for (int i = 0; i < kCcSpw; ++i) {
+      const int s = w + kCcWaves * i;
+      const float* row = a.data + (int64_t)(s < B ? s_row[s] : 0) * a.ldd;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int f = lane + 64 * j;
+        float v = (s < B && f < F) ? row[f] : 0.f;
+        if (flip_x && s < B && f < F) v = 1.0f - v;        // M:326
+        xr[i][j] = v;
+      }
+    }
+    for (int c0 = 0; c0 < C; c0 += kCcCg) {
+      float e[kCcSpw * kCcCg];                            // value i * CG + cc
+#pragma unroll
+      for (int q = 0; q < kCcSpw * kCcCg; ++q) e[q] = 0.f;
+#pragma unroll
+      for (int cc = 0; cc < kCcCg; ++cc) {
+        const int c = c0 + cc < C ? c0 + cc : C - 1;      // (a padding class repeats C-1)
+        const float* wc = a.W + (int64_t)c * F;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int f = lane + 64 * j;
+          const float wv = f < F ? wc[f] : 0.f;
+#pragma unroll
+          for (int i = 0; i < kCcSpw; ++i) e[i * kCcCg + cc] = fmaf(xr[i][j], wv, e[i * kCcCg + cc]);
+        }
+      }
+      transpose_reduce<64, kCcSpw * kCcCg>(e, lane);
+      // lanes 2v and 2v + 1 hold value row_of_lane(lane) (32 values over 64 lanes)
+      if ((lane & 1) == 0) {
+        const int v = row_of_lane<64, kCcSpw * kCcCg>(lane);
+        const int i = v / kCcCg, cc = v % kCcCg;
+        const int s = w + kCcWaves * i, c = c0 + cc;
+        if (s < B && c < C) s_z[s][c] = e[0] + a.b[c];
+      }
+    }
+    __syncthreads();
+
+    // ---- B: dz = d mean CE / dz, torch's log_softmax backward order
+    for (int s = w; s < B; s += kCcWaves) {
+      const bool cv = lane < C;
+      const float z = cv ? s_z[s][lane] : -INFINITY;
+      float m = z;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      float sum = cv ? expf(z - m) : 0.f;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+      const float logp = (z - m) - logf(sum);
+      const float gout = (lane == s_lab[s]) ? -invB : 0.f;
+      if (cv) s_z[s][lane] = gout - expf(logp) * (-invB);
+    }
+    __syncthreads();
+
+    // ---- C: gradient, SGD update (M:303) and the client's row; thread = 2 features,
+    // classes in groups of 16 (the batch columns are re-read per group from L1 / L2)
+    for (int c0 = 0; c0 < C; c0 += kCcCgC) {
+      float g[kCcFpt][kCcCgC];
+#pragma unroll
+      for (int h = 0; h < kCcFpt; ++h)
+#pragma unroll
+        for (int cc = 0; cc < kCcCgC; ++cc) g[h][cc] = 0.f;
+#pragma unroll 2
+      for (int s = 0; s < B; ++s) {
+        const float* row = a.data + (int64_t)s_row[s] * a.ldd;
+        float xv[kCcFpt];
+#pragma unroll
+        for (int h = 0; h < kCcFpt; ++h) {
+          const int f = tid + kCcThreads * h;
+          xv[h] = f < F ? row[f] : 0.f;
+          if (flip_x) xv[h] = 1.0f - xv[h];
+        }
+#pragma unroll
+        for (int cc = 0; cc < kCcCgC; ++cc) {
+          const float dz = s_z[s][c0 + cc];              // (columns >= C: never stored)
+#pragma unroll
+          for (int h = 0; h < kCcFpt; ++h) g[h][cc] = fmaf(dz, xv[h], g[h][cc]);
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < kCcFpt; ++h) {
+        const int f = tid + kCcThreads * h;
+        if (f < F) {
+#pragma unroll
+          for (int cc = 0; cc < kCcCgC; ++cc) {
+            const int c = c0 + cc;
+            if (c < C) {
+              float* wp = a.W + (int64_t)c * F + f;
+              const float p = *wp;
+              const float np = fmaf(-a.gamma, g[h][cc] + a.wd * p, p);
+              *wp = np;
+              put_param(a, k, (int64_t)c * F + f, np);
+            }
+          }
+        }
+      }
+    }
+    if (tid < C) {
+      const int c = tid;
+      float gb = 0.f;
+      for (int s = 0; s < B; ++s) gb += s_z[s][c];
+      const float p = a.b[c];
+      const float np = fmaf(-a.gamma, gb + a.wd * p, p);
+      a.b[c] = np;
+      put_param(a, k, (int64_t)C * F + c, np);
+    }
+    __syncthreads();   // W / b of this client before the next client's reads
+  }
+}
+
+bool client_chain_supported(int64_t F, int64_t C, int64_t B) {
+  return F >= 1 && F <= 64 * kCcNj && F <= kCcThreads * kCcFpt && C >= 1 && C <= kCcMaxC && B >= 1 &&
+         B <= kCcMaxB;
+}
+
+hipError_t launch_client_chain(const ClientChainArgs& a, hipStream_t s) {
+  // 13 features per lane: F <= 832 covers the reference's 28 x 28 inputs (MNIST and
+  // EMNIST, F = 784) without idle iterations; 16 per lane spilled 164 VGPRs
+  hipLaunchKernelGGL(client_chain<kCcNj>, dim3(1), dim3(kCcThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace gmk

@@ -166,6 +166,26 @@ hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_
                        double* part, double* score, float* out, int64_t* index, hipStream_t s,
                        int ws = 0);
 
+// The clients' local SGD chain of one federated step (clients.hip).
+struct ClientChainArgs {
+  const float* data;      // training set [n][ldd] fp32 (row = one flattened sample)
+  int64_t ldd;
+  const int64_t* labels;  // [n]
+  int64_t F, C;           // features, classes (the MLP's weight is [C][F])
+  const int* idx;         // [K][B] dataset rows of each client's batch
+  int64_t K, B, honest;
+  int attack;             // 0 none / weightflip, 1 classflip, 2 dataflip
+  float gamma, wd;
+  float* W;               // [C][F], updated in place (the model's weight)
+  float* b;               // [C]
+  float* X;               // client matrix: rows [K][ldx] or panels
+  int64_t ldx;            // rows: row stride
+  int64_t pstride;        // > 0: panels, elements between panels (panel width 1 << wshift)
+  int wshift;
+};
+bool client_chain_supported(int64_t F, int64_t C, int64_t B);
+hipError_t launch_client_chain(const ClientChainArgs& a, hipStream_t s);
+
 // OMA / synthetic fills (oma.hip).
 hipError_t launch_oma_apply(float* X, int64_t K, int64_t d, int64_t ldx, const float* hr,
                             const float* hi, const float* nr, const float* ni, hipStream_t s);

@@ -190,6 +190,85 @@ class ClientUpdates:
                 off += n
 
 
+class _ClientChain:
+    """The fused client steps (clients.hip, gm_client_chain_f32): the training set on the
+    device once, each step's batch indices from the reference's own samplers."""
+
+    ATTACK = {None: 0, "classflip": 1, "dataflip": 2, "weightflip": 0}
+
+    @classmethod
+    def make(cls, model, loss_func, train_dataset, cuts, batch, num_classes, device, mode):
+        if mode is False or device is None or torch.device(device).type != "cuda":
+            if mode is True:
+                raise ValueError("client_kernel=True needs a CUDA device")
+            return None
+        why = cls._unsupported(model, loss_func, train_dataset, batch, num_classes)
+        if why:
+            if mode is True:
+                raise ValueError(f"client_kernel=True: {why}")
+            return None
+        return cls(model, train_dataset, cuts, batch, num_classes, torch.device(device))
+
+    @staticmethod
+    def _linear(model):
+        m = model.module if isinstance(model, nn.DataParallel) else model
+        return m.linear if isinstance(m, MLP) else None
+
+    @classmethod
+    def _unsupported(cls, model, loss_func, ds, batch, num_classes):
+        lin = cls._linear(model)
+        if lin is None or lin.bias is None:
+            return "the model is not the reference's MLP (one nn.Linear with bias)"
+        if not (isinstance(loss_func, nn.CrossEntropyLoss) and loss_func.reduction == "mean"
+                and loss_func.weight is None and loss_func.label_smoothing == 0.0):
+            return "the loss is not CrossEntropyLoss(reduction='mean')"
+        if not isinstance(ds, torch.utils.data.TensorDataset) or len(ds.tensors) != 2:
+            return "the training set is not a TensorDataset(x, y)"
+        F, C = lin.in_features, lin.out_features
+        if C != num_classes or not (1 <= F <= 832 and 1 <= C <= 64 and 1 <= batch <= 64):
+            return f"unsupported shape (F={F}, C={C}, batch={batch})"
+        if lin.weight.dtype != torch.float32:
+            return "fp32 parameters only"
+        return None
+
+    def __init__(self, model, ds, cuts, batch, num_classes, device):
+        from . import _lib
+        from .aggregators import context
+        self.lib, self.ctx = _lib.load(), context(device)
+        self.lin = self._linear(model)
+        x, y = ds.tensors
+        self.x = x.reshape(x.shape[0], -1).to(device, torch.float32).contiguous()
+        self.y = y.to(device, torch.int64).contiguous()
+        self.F, self.C, self.B = self.lin.in_features, self.lin.out_features, batch
+        self.cuts = torch.tensor(cuts[:-1], dtype=torch.int32).unsqueeze(1)
+        self.device = device
+
+    def step(self, streams, clients, honest, attack_name, gamma, wd):
+        from . import _lib
+        from .aggregators import _stream_ptr
+        K = len(streams)
+        # the samplers' index lists, drawn in client order (a RandomSampler seeds its
+        # generator from the global one at its first draw, M:260-270)
+        local = torch.tensor([s._next_index() for s in streams], dtype=torch.int32)
+        if local.shape != (K, self.B):
+            raise RuntimeError("client batches must be full batches of batchSize samples")
+        idx = (local + self.cuts).to(self.device, non_blocking=True)
+        Wt, bt = self.lin.weight, self.lin.bias
+        if not (Wt.is_contiguous() and bt.is_contiguous()):
+            raise RuntimeError("the model's weight and bias must be contiguous")
+        X = clients.X
+        if clients.layout == "panels":
+            buf, ldx, lay = X.data, X.panel_stride, _lib.GM_LAYOUT_PANELS
+        else:
+            buf, ldx, lay = X, X.stride(0), _lib.GM_LAYOUT_ROWS
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.gm_client_chain_f32(
+                self.ctx.handle, self.x.data_ptr(), self.F, self.y.data_ptr(), self.F, self.C,
+                idx.data_ptr(), K, self.B, honest, self.ATTACK.get(attack_name, 0), float(gamma),
+                float(wd), Wt.data_ptr(), bt.data_ptr(), buf.data_ptr(), ldx, lay,
+                _stream_ptr(self.device)), "gm_client_chain_f32")
+
+
 # ---- the federated loop (row f4) ---------------------------------------------------
 
 def _log(*k):
@@ -200,9 +279,14 @@ def _log(*k):
 def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # noqa: N802
         byzantineSize=0, attack=None, rounds=10, displayInterval=1000, SEED=None,
         fixSeed=False, loss_func=None, train_dataset=None, validate_dataset=None, device=None,
-        batchSize=None, num_classes=10, verbose=True, layout="rows", eval_train=True, **kw):
+        batchSize=None, num_classes=10, verbose=True, layout="rows", eval_train=True,
+        client_kernel="auto", **kw):
     """Federated SGD with K = honest + Byzantine simulated clients (M:226-372).
     layout="panels" keeps the client matrix in the panel layout (every aggregator).
+    client_kernel="auto": on a GPU, with the reference's MLP, CrossEntropyLoss and a
+    TensorDataset, the K client steps of a federated step run as ONE HIP kernel
+    (gm_client_chain_f32) instead of K host-driven forward/backward passes; True
+    requires it, False keeps the per-client torch loop.
     EMNIST_Air_weight.py's variant: num_classes=62 (its MLP(784, 62) and 61 - y
     relabel, E:101, E:321) and eval_train=False (train loss / accuracy recorded as
     0, 0, E:273-274, E:364-365)."""
@@ -237,6 +321,8 @@ def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # 
     attack_name = attack.__name__ if attack is not None else None
     clients = ClientUpdates(model, K, layout=layout)
     params = clients.params
+    chain = _ClientChain.make(model, loss_func, train_dataset, cuts, batchSize, num_classes,
+                              device, client_kernel)
     is_gm = aggregate.__name__ == "gm"
     if noise_var is not None and not is_gm:
         from . import aggregators as _agg
@@ -246,7 +332,11 @@ def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # 
         fuse_oma = aggregate is _agg.gm2 and _agg._noise_source({}) == _agg._lib.GM_NOISE_PHILOX
     for r in range(rounds):
         for _ in range(displayInterval):
-            for node in range(K):
+            if chain is not None:
+                # the K clients' steps as one kernel (clients.hip): the same batches (the
+                # samplers' index streams, drawn in client order), the same chain
+                chain.step(streams, clients, honestSize, attack_name, gamma, weight_decay)
+            for node in (range(K) if chain is None else ()):
                 xb, yb = next(streams[node])
                 xb, yb = xb.to(device), yb.to(device)
                 if node >= honestSize and attack_name == "classflip":

@@ -247,6 +247,28 @@ int gm_oma_philox_panels_f32(gm_ctx* ctx, float* X, int64_t K, int64_t d, int64_
 int gm_rows_to_panels_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t ldx,
                           float* P, int64_t W, int64_t panel_stride, void* stream);
 
+/* The K clients' local SGD steps of one federated step (the loop body M:291-343:
+ * forward, CrossEntropyLoss (mean), backward, p -= gamma * (grad + weight_decay * p),
+ * the client's parameters copied out as its row), as one stream-ordered kernel, for the
+ * reference's linear model MLP(F, C) (M:53-61; F <= 832, C <= 64, batch B <= 64).
+ * The clients run in sequence on ONE model, as the reference's aliasing state_dict
+ * "snapshot" makes them (M:290, M:343): client k starts from client k-1's update, and
+ * W / b end as the last client's parameters (the aggregator's guess, M:349).
+ *   data     training samples [n][ldd] fp32 (device), labels [n] int64 (device)
+ *   idx      [K][B] int32 dataset rows of each client's batch (device): the reference's
+ *            RandomSampler draws (M:260-270), offset by the client's shard start
+ *   honest   clients k >= honest are Byzantine: attack 1 = classflip (target C-1-y,
+ *            M:320), 2 = dataflip (input 1-x, M:326), 0 = none (also weightflip,
+ *            which rewrites the matrix afterwards, M:380-383)
+ *   W, b     the model's weight [C][F] and bias [C] (device), updated in place
+ *   X        the client matrix: row k = [W (C*F, row-major), b (C)], layout
+ *            GM_LAYOUT_ROWS (ldx = row stride >= C*F + C) or GM_LAYOUT_PANELS
+ *            (ldx = panel stride >= K*W, W = gm_panel_width(K)). */
+int gm_client_chain_f32(gm_ctx* ctx, const float* data, int64_t ldd, const int64_t* labels,
+                        int64_t F, int64_t C, const int32_t* idx, int64_t K, int64_t B,
+                        int64_t honest, int32_t attack, float gamma, float weight_decay,
+                        float* W, float* b, float* X, int64_t ldx, int32_t layout, void* stream);
+
 /* OMA with the reference's own draws (device arrays): h_re[K], h_im[K],
  * n_re[K*d], n_im[K*d] (row-major, already scaled by sqrt(noise_var)).
  * Bit-exact with the reference's fp32 op order. */

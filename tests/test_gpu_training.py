@@ -154,3 +154,90 @@ def test_loop_more_attacks_device_resident(attack, var, name, layout, monkeypatc
     np.testing.assert_allclose(tl, meta["trainLossPath"], rtol=1e-4)
     np.testing.assert_allclose(vl, meta["valLossPath"], rtol=1e-4)
     np.testing.assert_allclose([float(v) for v in vv], meta["variencePath"], rtol=1e-4)
+
+
+def _chain_reference(x, y, idx, W, b, honest, attack, gamma, wd, C):
+    """The reference's client loop body (M:291-343) in float64 torch with autograd:
+    client k starts from client k-1's parameters (the aliasing snapshot, M:290/343)."""
+    W, b = W.double().clone(), b.double().clone()
+    rows = []
+    for k in range(idx.shape[0]):
+        xb, yb = x[idx[k].long()].double(), y[idx[k].long()].clone()
+        if k >= honest and attack == 1:
+            yb = (C - 1) - yb
+        if k >= honest and attack == 2:
+            xb = 1.0 - xb
+        Wv, bv = W.clone().requires_grad_(), b.clone().requires_grad_()
+        loss = torch.nn.functional.cross_entropy(xb @ Wv.T + bv, yb)
+        loss.backward()
+        with torch.no_grad():
+            W = W - gamma * (Wv.grad + wd * W)
+            b = b - gamma * (bv.grad + wd * b)
+        rows.append(torch.cat([W.flatten(), b]))
+    return torch.stack(rows), W, b
+
+
+@pytest.mark.parametrize("C", [10, 62])
+@pytest.mark.parametrize("attack", [0, 1, 2])
+@pytest.mark.parametrize("layout", ["rows", "panels"])
+def test_client_chain_kernel_vs_fp64(C, attack, layout):
+    """gm_client_chain_f32 (clients.hip) against the loop body in float64: every client's
+    row of the client matrix and the final W / b (the last client's, M:349)."""
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd import _lib
+    from byzantine_aircomp_amd.panels import ClientPanels
+    g = torch.Generator().manual_seed(C * 10 + attack)
+    n, F, K, B, honest = 3000, 784, 12, 50, 9
+    x = (0.3 * torch.randn(n, F, generator=g)).cuda()
+    y = torch.randint(0, C, (n,), generator=g).cuda()
+    idx = torch.randint(0, n, (K, B), generator=g, dtype=torch.int32).cuda()
+    W0 = (0.05 * torch.randn(C, F, generator=g)).cuda()
+    b0 = torch.full((C,), 0.01).cuda()
+    d = C * F + C
+    want, Ww, bw = _chain_reference(x.cpu(), y.cpu(), idx.cpu(), W0.cpu(), b0.cpu(), honest,
+                                    attack, 1e-2, 1e-3, C)
+    W, b = W0.clone(), b0.clone()
+    if layout == "panels":
+        Xp = ClientPanels(K, d)
+        buf, ldx, lay = Xp.data, Xp.panel_stride, _lib.GM_LAYOUT_PANELS
+    else:
+        Xr = torch.full((K, d + 3), float("nan"), device="cuda")
+        buf, ldx, lay = Xr, d + 3, _lib.GM_LAYOUT_ROWS
+    ctx = bz.context()
+    _lib.check(ctx.lib.gm_client_chain_f32(ctx.handle, x.data_ptr(), F, y.data_ptr(), F, C,
+                                           idx.data_ptr(), K, B, honest, attack, 1e-2, 1e-3,
+                                           W.data_ptr(), b.data_ptr(), buf.data_ptr(), ldx, lay,
+                                           torch.cuda.current_stream().cuda_stream), "chain")
+    torch.cuda.synchronize()
+    got = Xp.to_rows() if layout == "panels" else Xr[:, :d]
+    assert rel_l2(got.cpu().numpy(), want.numpy()) <= 1e-6
+    for k in range(K):
+        assert rel_l2(got[k].cpu().numpy(), want[k].numpy()) <= 1e-6, k
+    assert rel_l2(W.cpu().numpy(), Ww.numpy()) <= 1e-6
+    assert rel_l2(b.cpu().numpy(), bw.numpy()) <= 1e-6
+
+
+@pytest.mark.parametrize("layout", ["rows", "panels"])
+def test_loop_client_kernel_equals_torch_loop(layout):
+    """SGD with the fused client steps vs the per-client torch loop on the GPU: the
+    same batches (sampler draws in the reference's order) and records to fp32 rounding."""
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd import training as T
+    tr = torch.utils.data.TensorDataset(*synthetic_mnist(601, 2000))
+    va = torch.utils.data.TensorDataset(*synthetic_mnist(602, 500))
+    out = []
+    for ck in (True, False):
+        model = T.modelFactory(SEED=2021).cuda()
+        res = T.SGD(model, gamma=1e-2, aggregate=bz.gm2, weight_decay=0.0, honestSize=45,
+                    byzantineSize=5, attack=T.classflip, rounds=2, displayInterval=3, SEED=2021,
+                    fixSeed=True, loss_func=torch.nn.CrossEntropyLoss(), train_dataset=tr,
+                    validate_dataset=va, device=torch.device("cuda"), batchSize=50,
+                    verbose=False, layout=layout, client_kernel=ck)
+        out.append(res)
+    (m1, tl1, _, vl1, _, v1), (m2, tl2, _, vl2, _, v2) = out
+    w1 = torch.cat([p.detach().flatten() for p in m1.parameters()]).cpu().numpy()
+    w2 = torch.cat([p.detach().flatten() for p in m2.parameters()]).cpu().numpy()
+    assert rel_l2(w1, w2) <= 1e-5
+    np.testing.assert_allclose(tl1, tl2, rtol=1e-5)
+    np.testing.assert_allclose(vl1, vl2, rtol=1e-5)
+    np.testing.assert_allclose([float(v) for v in v1], [float(v) for v in v2], rtol=1e-4)

@@ -43,9 +43,10 @@ def main():
           displayInterval=3, SEED=2021, fixSeed=True, loss_func=torch.nn.CrossEntropyLoss(),
           train_dataset=tr, validate_dataset=va, device=dev, batchSize=50, verbose=False,
           eval_train=False)
-    for agg_name, var, layout in (("gm", 1e-2, "rows"), ("gm2", None, "rows"), ("gm2", 1e-2, "rows"),
-                                  ("gm2", None, "panels"), ("median", None, "rows"),
-                                  ("Krum", None, "rows")):
+    for agg_name, var, layout, ck in (("gm", 1e-2, "rows", True), ("gm", 1e-2, "rows", False),
+                                      ("gm2", None, "rows", True), ("gm2", None, "rows", False),
+                                      ("gm2", 1e-2, "rows", True), ("gm2", None, "panels", True),
+                                      ("median", None, "rows", True), ("Krum", None, "rows", True)):
         base = getattr(bz, agg_name)
         agg_t = [0.0, 0]
 
@@ -68,11 +69,12 @@ def main():
               byzantineSize=5, attack=T.classflip, rounds=1, displayInterval=a.steps, SEED=2021,
               fixSeed=True, loss_func=torch.nn.CrossEntropyLoss(), train_dataset=tr,
               validate_dataset=va, device=dev, batchSize=50, verbose=False, layout=layout,
-              eval_train=False)
+              eval_train=False, client_kernel=ck)
         torch.cuda.synchronize(dev)
         total = time.perf_counter() - t0
         line = {"what": "training.SGD step (K=50: 45 honest + 5 classflip, MLP d=7850)",
                 "agg": agg_name, "var": var, "layout": layout, "steps": a.steps,
+                "client_steps": "one HIP kernel (clients.hip)" if ck else "torch, per client",
                 "ms_per_step": 1e3 * total / a.steps,
                 "agg_ms_per_step": (1e3 * agg_t[0] / agg_t[1]) if agg_t[1] else None,
                 "note": "includes one validation pass (500 samples) per run"}
