@@ -155,24 +155,41 @@ def pmc_traffic(workload, layout, kernel="weiszfeld_pass", mode="0"):
     return None, None
 
 
-def fixed_point_step(X: torch.Tensor, g: torch.Tensor, allreduce=None, rows=64):
+def columns(src, c0, c1):
+    """Columns [c0, c1) of a [K, d] client matrix held as a row-major tensor or in the
+    panel layout (ClientPanels: c0 a multiple of the panel width), as a [K, c1 - c0] tensor."""
+    if isinstance(src, torch.Tensor):
+        return src[:, c0:c1]
+    W = src.W
+    p0, p1 = c0 // W, -(-c1 // W)
+    blk = src.data[p0:p1].permute(1, 0, 2).reshape(src.K, (p1 - p0) * W)
+    return blk[:, c0 - p0 * W:c1 - p0 * W]
+
+
+def fixed_point_step(X, g: torch.Tensor, allreduce=None, cols=1 << 20):
     """fp64 Weiszfeld step at g over this rank's columns (all ranks' sums combined by
     `allreduce`): returns (||T(g) - g||, ||g||) with T the gm2 map (M:174-179).  At a
     converged aggregate ||T(g) - g|| is of the order of the reference's last movement
-    (<= tol = 1e-5); a wrong aggregate shows up as a large step."""
-    K = X.shape[0]
+    (<= tol = 1e-5); a wrong aggregate shows up as a large step.  X: a row-major [K, d]
+    tensor or a ClientPanels, read in column slices (bounded fp64 temporaries)."""
+    K, d = X.shape
+    if not isinstance(X, torch.Tensor):
+        cols = max(X.W, cols // X.W * X.W)
     gd = g.double()
-    d2 = torch.zeros(K, dtype=torch.float64, device=X.device)
-    for k0 in range(0, K, rows):
-        d2[k0:k0 + rows] = ((X[k0:k0 + rows].double() - gd) ** 2).sum(1)
+    d2 = torch.zeros(K, dtype=torch.float64, device=g.device)
+    for c0 in range(0, d, cols):
+        c1 = min(d, c0 + cols)
+        d2 += ((columns(X, c0, c1).double() - gd[c0:c1]) ** 2).sum(1)
     if allreduce:
         allreduce(d2)
     w = 1.0 / d2.sqrt().clamp_min(1e-4)
-    step = torch.zeros_like(gd)
-    for k0 in range(0, K, rows):
-        step += (w[k0:k0 + rows, None] * (X[k0:k0 + rows].double() - gd)).sum(0)
-    step /= w.sum()
-    nums = torch.stack([(step ** 2).sum(), (gd ** 2).sum()])
+    nums = torch.zeros(2, dtype=torch.float64, device=g.device)
+    ws = w.sum()
+    for c0 in range(0, d, cols):
+        c1 = min(d, c0 + cols)
+        step = (w[:, None] * (columns(X, c0, c1).double() - gd[c0:c1])).sum(0) / ws
+        nums[0] += (step ** 2).sum()
+        nums[1] += (gd[c0:c1] ** 2).sum()
     if allreduce:
         allreduce(nums)
     return math.sqrt(float(nums[0])), math.sqrt(float(nums[1]))
@@ -189,7 +206,9 @@ def cpu_baseline(X, g0, agg, var, iters, d_full, budget, max_cols):
     torch.set_num_threads(threads)
     try:
         dc = min(max_cols, X.shape[1])
-        Xc, gc = X[:, :dc].contiguous().cpu(), g0[:dc].contiguous().cpu()
+        if not isinstance(X, torch.Tensor):
+            dc = max(X.W, dc // X.W * X.W)
+        Xc, gc = columns(X, 0, dc).contiguous().cpu(), g0[:dc].contiguous().cpu()
         fn = (lambda n: orc.gm2(Xc, {"maxiter": n, "tol": -1.0, "guess": gc})) if agg == "gm2" \
             else (lambda n: orc.gm(Xc, {"maxiter": n, "tol": -1.0, "guess": gc, "noise_var": var,
                                         "P_max": 1}))
@@ -249,26 +268,36 @@ def run_c5(args, json_out, rank=0, world=1):
     # row-major fill, untimed
     from byzantine_aircomp_amd.batched import ProblemPanels
     use_panels = args.layout in ("auto", "panels")
-    groups = []                      # (var, X [P, K, d], g0 [P, d], panels or None)
+    # (var, rows X [P, K, d] or None, g0 [P, d], panels or None).  With panels no row-major
+    # copy is kept: each problem is generated into one [K, d] scratch matrix and packed
+    # (the sweep's resident footprint is the 82 GB of problems, not twice that)
+    groups = []
+    tmp = torch.empty(K, d, device=dev) if use_panels else None
     for vi, var in enumerate(C5_VARS):
         for c0 in range(0, per_var, chunk):
             P = min(chunk, per_var - c0)
-            groups.append((vi, var, c0, torch.empty(P, K, d, device=dev),
+            groups.append((vi, var, c0, None if use_panels else torch.empty(P, K, d, device=dev),
                            torch.empty(P, d, device=dev),
                            ProblemPanels(P, K, d, device=dev) if use_panels else None))
 
+    def fill_problem(vi, c0, p, dst):
+        B = C5_BYZ[(c0 + p) % 3]
+        _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, dst.data_ptr(), K, d, d, B, 0.0,
+                                               0.05, 0.25, 0.5, rs + 1000 * vi + c0 + p,
+                                               stream), "fill")
+
     def fill():
-        for vi, var, c0, X, g0, _ in groups:
-            for p in range(X.shape[0]):
-                B = C5_BYZ[(c0 + p) % 3]
-                _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, X[p].data_ptr(), K, d, d, B, 0.0,
-                                                       0.05, 0.25, 0.5, rs + 1000 * vi + c0 + p,
-                                                       stream), "fill")
+        for vi, var, c0, X, g0, Pn in groups:
+            for p in range(g0.shape[0]):
+                if Pn is None:
+                    fill_problem(vi, c0, p, X[p])
+                else:
+                    fill_problem(vi, c0, p, tmp)
+                    _lib.check(ctx.lib.gm_rows_to_panels_f32(
+                        ctx.handle, tmp.data_ptr(), K, d, d, Pn.data[p].data_ptr(), Pn.W,
+                        Pn.panel_stride, stream), "pack")
             _lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), g0.numel(), 0.0, 0.01,
                                                   rs + 777 + vi + c0, stream), "fill")
-        for *_, X, _g, Pn in groups:
-            if Pn is not None:
-                Pn.copy_rows_(X)
         torch.cuda.synchronize(dev)
 
     outs = {}                        # the last step's aggregates per group (for `check`)
@@ -345,7 +374,12 @@ def run_c5(args, json_out, rank=0, world=1):
     traffic, traffic_src = pmc_traffic("c5", "panels" if use_panels else "rows")
     cpu = None
     if not args.no_cpu and world == 1:
-        cpu = c5_cpu_baseline(groups[0][3][0], groups[0][4][0], mean_it, n_prob, args.cpu_budget)
+        vi0, _, c00, X0, g00, _ = groups[0]
+        if X0 is None:                       # problem 0's clean rows, regenerated
+            fill_problem(vi0, c00, 0, tmp)
+            torch.cuda.synchronize(dev)
+        cpu = c5_cpu_baseline(tmp if X0 is None else X0[0], g00[0], mean_it, n_prob,
+                              args.cpu_budget)
     line = {
         "metric": METRIC, "value": world * n_prob * args.steps / total, "unit": "aggregations/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -513,9 +547,37 @@ def main():
         lo, hi = 0, d_total
     d = hi - lo
 
-    X = torch.empty(K, d, dtype=torch.float32, device=dev)
-    _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, X.data_ptr(), K, d, d, B, 0.0, 0.05, 0.25,
-                                           0.5, 20211, stream), "fill")
+    layout = args.layout
+    if layout == "auto":
+        layout = "panels" if (args.workload.startswith("c3") and args.algo in ("auto", "stream")) \
+            or (args.workload.startswith("c4") and args.algo in ("auto", "stream", "gram")) \
+            else "rows"
+    # a panel-layout input whose row-major copy would not fit beside it (the whole C4 job,
+    # 256 x 125M = 128 GB, on one GPU) is generated straight into the panels, column slice
+    # by column slice through a scratch matrix: no rows copy, no rows-layout measurement
+    big = layout == "panels" and 8.0 * K * d > 120e9
+    panels = None
+    if big:
+        panels = bz.ClientPanels(K, d, device=dev)
+        S = panels.W * 8192
+        tmp = torch.empty(K, S, dtype=torch.float32, device=dev)
+        fctx = bz.aggregators.Context(dev.index)       # its shard offset keys the columns
+        for c0 in range(0, d, S):
+            n = min(S, d - c0)
+            fctx.set_shard(d_total, lo + c0)
+            _lib.check(ctx.lib.gm_fill_clients_f32(fctx.handle, tmp.data_ptr(), K, n, S, B, 0.0,
+                                                   0.05, 0.25, 0.5, 20211, stream), "fill")
+            _lib.check(ctx.lib.gm_rows_to_panels_f32(fctx.handle, tmp.data_ptr(), K, n, S,
+                                                     panels.data[c0 // panels.W].data_ptr(),
+                                                     panels.W, panels.panel_stride, stream), "pack")
+        torch.cuda.synchronize(dev)
+        fctx.close()
+        del tmp
+        X = None
+    else:
+        X = torch.empty(K, d, dtype=torch.float32, device=dev)
+        _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, X.data_ptr(), K, d, d, B, 0.0, 0.05,
+                                               0.25, 0.5, 20211, stream), "fill")
     g0 = torch.empty(d, dtype=torch.float32, device=dev)
     _lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), d, 0.0, 0.01, 20212, stream),
                "fill")
@@ -532,13 +594,6 @@ def main():
 
         def last():
             return bz.aggregators.last_result
-    layout = args.layout
-    if layout == "auto":
-        layout = "panels" if (args.workload.startswith("c3") and args.algo in ("auto", "stream")) \
-            or (args.workload.startswith("c4") and args.algo in ("auto", "stream", "gram")) \
-            else "rows"
-    panels = None
-
     def inputs(lay):
         nonlocal panels
         if lay == "rows":
@@ -590,7 +645,7 @@ def main():
     alt = None
     alt_layout = "rows" if layout == "panels" else "panels"
     alt_steps = args.alt_steps if args.alt_steps is not None else max(3, args.steps // 4)
-    if alt_steps > 0 and (alt_layout == "rows" or (args.algo in ("auto", "stream", "gram")
+    if alt_steps > 0 and not big and (alt_layout == "rows" or (args.algo in ("auto", "stream", "gram")
                                                    and bz.panel_width(K) > 0
                                                    and d_total >= 1 << 20)):
         a_el, a_ms, a_n, a_res, _ = measure(inputs(alt_layout), alt_steps, 1)
@@ -602,12 +657,13 @@ def main():
                "frac": 4.0 * K * d / a_pass / 1e9 / HBM_PEAK_GBS,
                "aggregation_frac": a_passes * 4.0 * K * d / (a_el / alt_steps) / 1e9
                / HBM_PEAK_GBS}
+    src = panels if big else X          # the matrix the checks read
     panels = None
 
     # full-size correctness: the fp64 fixed-point step at the returned aggregate
     check = None
     if not args.no_check and agg_name == "gm2":
-        step, gn = fixed_point_step(X, out, allreduce)
+        step, gn = fixed_point_step(src, out, allreduce)
         check = {"what": "fp64 gm2 step ||T(g) - g|| at the returned g over the full K x d "
                          "(T = M:174-179); the reference stops at movement <= tol = 1e-5",
                  "fixed_point_step": step, "g_norm": gn, "relative": step / max(gn, 1e-300),
@@ -713,7 +769,11 @@ def main():
                                    + (f", noise_var {var}" if agg_name == "gm" else ""),
                        "K": K, "d": d_total, "d_local": d, "byzantine": B, "iters": res.iters,
                        "algo": res.algo, "gram_guard": res.guard, "layout": layout,
-                       "parallelism": parallelism, "passes_per_aggregation": passes},
+                       "parallelism": parallelism, "passes_per_aggregation": passes,
+                       "input": ("generated straight into the panel layout (no row-major copy "
+                                 "resident: it would not fit beside the panels)") if big else
+                                "row-major fill, packed to panels once (untimed)"
+                                if layout == "panels" else "row-major"},
             "roofline": roof,
             "cpu_baseline": None,
             "check": check,
@@ -721,7 +781,7 @@ def main():
             "soak": soak,
         }
         if world == 1 and not args.no_cpu and not args.rehearse_shard:
-            line["cpu_baseline"] = cpu_baseline(X, g0, agg_name, var, res.iters, d_total,
+            line["cpu_baseline"] = cpu_baseline(src, g0, agg_name, var, res.iters, d_total,
                                                 args.cpu_budget, args.cpu_d)
         print(json.dumps(line), file=json_out, flush=True)
     torch.cuda.synchronize(dev)
