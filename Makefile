@@ -32,15 +32,20 @@ clean:
 
 .PHONY: all clean
 
-# A/B build: the streaming pass with the two-tile PIPE schedule compiled in
-# (GMAGG_PASS_VARIANT=1 selects it; GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so
-# loads this library at run time).
-ALT := byzantine_aircomp_amd/libgmagg_alt.so
-$(BUILD)/alt/stream_pass.o: $(CSRC)/stream_pass.hip $(HDRS)
+# A/B build: every object compiled again with ALT_FLAGS into build/alt, linked as
+# byzantine_aircomp_amd/libgmagg_alt.so; GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so
+# loads it at run time (tools/ab.py --variant alt=GMAGG_LIB=...).
+#   make alt ALT_FLAGS=-DGMK_H16_SHAPE=16
+ALT       := byzantine_aircomp_amd/libgmagg_alt.so
+ALT_FLAGS ?= -DGMK_PIPE_VARIANT
+ALT_OBJS  := $(patsubst $(CSRC)/%.hip,$(BUILD)/alt/%.o,$(SRCS))
+$(BUILD)/alt/gram.o: HIPFLAGS += -fno-slp-vectorize
+$(BUILD)/alt/%.o: $(CSRC)/%.hip $(HDRS) FORCE
 	@mkdir -p $(BUILD)/alt
-	$(HIPCC) $(HIPFLAGS) -DGMK_PIPE_VARIANT -c $< -o $@
-$(ALT): $(BUILD)/alt/stream_pass.o $(filter-out $(BUILD)/stream_pass.o,$(OBJS))
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl \
+	$(HIPCC) $(HIPFLAGS) $(ALT_FLAGS) -c $< -o $@
+$(ALT): $(ALT_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(ALT_OBJS) -L/opt/rocm/lib -lrccl \
 	    -Wl,-rpath,/opt/rocm/lib
 alt: $(ALT)
-.PHONY: alt
+FORCE:
+.PHONY: alt FORCE

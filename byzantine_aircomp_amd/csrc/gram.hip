@@ -631,6 +631,80 @@ __device__ __forceinline__ void h16_step(const _Float16* Lh, const _Float16* Lm,
   h16_step_b<KT, W, KT - 1>(Lh, Lm, off, haw, maw, hao, mao, acc);
 }
 
+// The same tiles on v_mfma_f32_16x16x32_f16 (GMK_H16_SHAPE == 16; A/B builds): each
+// 32 x 32 tile as 2 x 2 sub-tiles of 16 x 16, one 32-column k-step per MFMA.  The same
+// cycles per FLOP as 32x32x16; the chip holds a higher clock on the 16x16 shape under
+// load (MI355X_MICROARCH.md 'DVFS give-back' item 7).  Fragment of rows R0..R0+15,
+// k-step columns c..c+31: lane l holds row R0 + (l & 15), columns c + 8 (l >> 4) .. +7.
+#ifndef GMK_H16_SHAPE
+#define GMK_H16_SHAPE 32
+#endif
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+template <int KT, int W, int B>
+__device__ __forceinline__ void h16s_step_b(const _Float16* Lh, const _Float16* Lm, int off,
+                                            const f16x8 (&ha)[2], const f16x8 (&ma)[2],
+                                            const f16x8 (&ho)[2], const f16x8 (&mo)[2],
+                                            f32x4v (&acc)[GramShape<KT>::PER_WAVE][4]) {
+  if constexpr (B >= W) {
+    using O = H16Order<KT, W>;
+    f16x8 hb[2], mb[2];
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      hb[sb] = *reinterpret_cast<const f16x8*>(Lh + (B * 32 + 16 * sb) * kH16LS + off);
+      mb[sb] = *reinterpret_cast<const f16x8*>(Lm + (B * 32 + 16 * sb) * kH16LS + off);
+    }
+    constexpr int tw = O::slot_w(B);
+#pragma unroll
+    for (int sa = 0; sa < 2; ++sa)
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        f32x4v& c = acc[tw][sa * 2 + sb];
+        if constexpr (GMK_H16_DIAG && B == W) {
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha[sa], hb[sb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha[sa], mb[sb] + mb[sb], c, 0, 0, 0);
+        } else {
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha[sa], hb[sb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha[sa], mb[sb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ma[sa], hb[sb], c, 0, 0, 0);
+        }
+      }
+    if constexpr (KT > 1 && B >= KT - 1 - W) {
+      constexpr int to = O::slot_o(B);
+#pragma unroll
+      for (int sa = 0; sa < 2; ++sa)
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb) {
+          f32x4v& c = acc[to][sa * 2 + sb];
+          if constexpr (GMK_H16_DIAG && B == KT - 1 - W) {
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ho[sa], hb[sb], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ho[sa], mb[sb] + mb[sb], c, 0, 0, 0);
+          } else {
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ho[sa], hb[sb], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ho[sa], mb[sb], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(mo[sa], hb[sb], c, 0, 0, 0);
+          }
+        }
+    }
+    h16s_step_b<KT, W, B - 1>(Lh, Lm, off, ha, ma, ho, mo, acc);
+  }
+}
+
+template <int KT, int W>
+__device__ __forceinline__ void h16s_step(const _Float16* Lh, const _Float16* Lm, int off,
+                                          f32x4v (&acc)[GramShape<KT>::PER_WAVE][4]) {
+  constexpr int AO = KT == 1 ? 0 : KT - 1 - W;
+  f16x8 ha[2], ma[2], ho[2], mo[2];
+#pragma unroll
+  for (int sa = 0; sa < 2; ++sa) {
+    ha[sa] = *reinterpret_cast<const f16x8*>(Lh + (W * 32 + 16 * sa) * kH16LS + off);
+    ma[sa] = *reinterpret_cast<const f16x8*>(Lm + (W * 32 + 16 * sa) * kH16LS + off);
+    ho[sa] = *reinterpret_cast<const f16x8*>(Lh + (AO * 32 + 16 * sa) * kH16LS + off);
+    mo[sa] = *reinterpret_cast<const f16x8*>(Lm + (AO * 32 + 16 * sa) * kH16LS + off);
+  }
+  h16s_step_b<KT, W, KT - 1>(Lh, Lm, off, ha, ma, ho, mo, acc);
+}
+
 // Producer waves (4..7): stream every stage into the LDS images, two stages of
 // loads in flight (rolling re-issue).  Three sets fit the 256 VGPRs of a
 // two-waves-per-SIMD block only without the unroll by 6 that static set indices
@@ -752,6 +826,62 @@ __device__ __forceinline__ void h16_consumer(int nstage, int nseg, float* __rest
     for (; seg < nseg; ++seg) flush(seg, true);              // blocks with fewer stages
 }
 
+// h16_consumer on the 16x16x32 shape: the same slab format (every 32 x 32 tile written
+// in the 32x32 accumulator's element order, so gram_reduce_* are unchanged).
+template <int KT, int W, int DBG>
+__device__ __forceinline__ void h16s_consumer(int nstage, int nseg, float* __restrict__ slab,
+                                              H16Lds<KT>& lds, const int* s_exp) {
+  using Sh = GramShape<KT>;
+  constexpr int NT = Sh::PER_WAVE;
+  constexpr bool MMA = W >= 0 && DBG != 1;
+  constexpr int WW = W < 0 ? 0 : W;
+  const int lane = threadIdx.x & 63;
+  f32x4v acc[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[t][q] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  float* base = slab + (int64_t)blockIdx.x * nseg * Sh::TILES * 1024;
+  auto flush = [&](int seg, bool zero) {
+    float* out = base + (int64_t)seg * Sh::TILES * 1024;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      int a, b;
+      wave_tile<KT>(WW, t, a, b);
+      float* o = out + tri_index(a, b, KT) * 1024;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int sa = q >> 1, sb = q & 1;
+        const int C = 16 * sb + (lane & 15);                   // column in the 32x32 tile
+        const int ec = s_exp[b * 32 + C];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int R = 16 * sa + 4 * (lane >> 4) + r;          // row in the 32x32 tile
+          const int e = ((R & 3) + 4 * (R >> 3)) * 64 + C + 32 * ((R >> 2) & 1);
+          o[e] = zero ? 0.f : ldexpf(acc[t][q][r], -(s_exp[a * 32 + R] + ec));
+        }
+        acc[t][q] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  const int fo = (lane & 15) * kH16LS + (lane >> 4) * 8;   // fragment offset in a sub-tile
+  __syncthreads();                                           // the producers' scale exchange
+  __syncthreads();                                           // stage 0 is in buffer 0
+  int seg = 0;
+  for (int s = 0; s < nstage; ++s) {
+    if constexpr (MMA) {
+      const _Float16* Lh = lds[s & 1][0];
+      const _Float16* Lm = lds[s & 1][1];
+#pragma unroll
+      for (int ks = 0; ks < kH16BK / 32; ++ks) h16s_step<KT, WW>(Lh, Lm, ks * 32 + fo, acc);
+      if ((s + 1) % kH16Flush == 0 || s + 1 == nstage) flush(seg++, false);
+    }
+    __syncthreads();
+  }
+  if constexpr (MMA)
+    for (; seg < nseg; ++seg) flush(seg, true);
+}
+
 template <int KT, int DBG, int WS>
 __global__ void __launch_bounds__(512, 1) gram_h16_partial(const float* __restrict__ X, int64_t K,
                                                            int64_t d, int64_t ldx, int64_t pstride,
@@ -769,23 +899,29 @@ __global__ void __launch_bounds__(512, 1) gram_h16_partial(const float* __restri
     h16_producer<KT, DBG, WS>(X, K, ldx, pstride, p, c_begin, c_end, nstage, lds, s_exp, s_bmax);
     return;
   }
+#if GMK_H16_SHAPE == 16
+#define GMK_H16_CONSUMER h16s_consumer
+#else
+#define GMK_H16_CONSUMER h16_consumer
+#endif
   if constexpr (KT == 8) {
     switch (w) {
-      case 0: h16_consumer<KT, 0, DBG>(nstage, nseg, slab, lds, s_exp); break;
-      case 1: h16_consumer<KT, 1, DBG>(nstage, nseg, slab, lds, s_exp); break;
-      case 2: h16_consumer<KT, 2, DBG>(nstage, nseg, slab, lds, s_exp); break;
-      default: h16_consumer<KT, 3, DBG>(nstage, nseg, slab, lds, s_exp); break;
+      case 0: GMK_H16_CONSUMER<KT, 0, DBG>(nstage, nseg, slab, lds, s_exp); break;
+      case 1: GMK_H16_CONSUMER<KT, 1, DBG>(nstage, nseg, slab, lds, s_exp); break;
+      case 2: GMK_H16_CONSUMER<KT, 2, DBG>(nstage, nseg, slab, lds, s_exp); break;
+      default: GMK_H16_CONSUMER<KT, 3, DBG>(nstage, nseg, slab, lds, s_exp); break;
     }
   } else if constexpr (KT == 4) {
     switch (w) {
-      case 0: h16_consumer<KT, 0, DBG>(nstage, nseg, slab, lds, s_exp); break;
-      case 1: h16_consumer<KT, 1, DBG>(nstage, nseg, slab, lds, s_exp); break;
-      default: h16_consumer<KT, -1, DBG>(nstage, nseg, slab, lds, s_exp); break;
+      case 0: GMK_H16_CONSUMER<KT, 0, DBG>(nstage, nseg, slab, lds, s_exp); break;
+      case 1: GMK_H16_CONSUMER<KT, 1, DBG>(nstage, nseg, slab, lds, s_exp); break;
+      default: GMK_H16_CONSUMER<KT, -1, DBG>(nstage, nseg, slab, lds, s_exp); break;
     }
   } else {
-    if (w == 0) h16_consumer<KT, 0, DBG>(nstage, nseg, slab, lds, s_exp);
-    else h16_consumer<KT, -1, DBG>(nstage, nseg, slab, lds, s_exp);
+    if (w == 0) GMK_H16_CONSUMER<KT, 0, DBG>(nstage, nseg, slab, lds, s_exp);
+    else GMK_H16_CONSUMER<KT, -1, DBG>(nstage, nseg, slab, lds, s_exp);
   }
+#undef GMK_H16_CONSUMER
 }
 
 // Sum the fp32 block partials in fp64 in a fixed order, in two steps so that
