@@ -46,7 +46,7 @@ struct Tile {
 // it fits the 32-bit lane offset, and the HBM stream is sequential.
 template <int V, int NW, int LPR, int R, int MODE, int SCHED, int OCC = 1, bool PANEL = false>
 __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs a) {
-  constexpr bool PIPE = SCHED == 1, ROLL = SCHED == 2;
+  constexpr bool PIPE = SCHED == 1, ROLL = SCHED == 2 || SCHED == 3, ROLL2 = SCHED == 3;
   constexpr bool SUM_ONLY = MODE == 3;     // closing pass of the Gram variant: g = sum c_k x_k
   constexpr bool OMA_INIT = MODE == 4;
   constexpr bool INIT = MODE == 1 || MODE == 2 || OMA_INIT;
@@ -312,6 +312,19 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
       fetch(ch + 2 * grid, ta);
       process(ch + grid, tb, -1);
     }
+  } else if constexpr (ROLL2) {
+    // two tiles, each rolled two grid strides ahead: chunks c+1 and c+2 in flight while
+    // c is reduced (for passes whose blocks are latency-bound on too few bytes in flight:
+    // small chunks, C5's K = 50 x 128 panels)
+    T ta, tb;
+    int64_t ch = blockIdx.x;
+    fetch(ch, ta);
+    fetch(ch + grid, tb);
+    for (; ch < nch; ch += 2 * grid) {
+      process(ch, ta, ch + 2 * grid);
+      if (ch + grid >= nch) break;       // block-uniform
+      process(ch + grid, tb, ch + 3 * grid);
+    }
   } else if constexpr (ROLL) {
     T t;
     fetch(blockIdx.x, t);
@@ -360,7 +373,8 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
 
 // ---------------------------------------------------------------------------
 // Launch plumbing.  GMAGG_PASS_VARIANT: -1 auto (default), 0 plain, 1 pipelined
-// (-DGMK_PIPE_VARIANT builds only), 2 rolling prefetch.
+// (-DGMK_PIPE_VARIANT builds only), 2 rolling prefetch, 3 two tiles rolled two chunks
+// ahead (panels).
 
 static int pass_variant() {
   static const int v = [] {
@@ -383,6 +397,8 @@ static const void* pass_fn(bool panel) {
   if constexpr (V == 4) {
     if (panel) {
       const int pv = pass_variant();
+      if (pv == 3)
+        return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 3, OCC, true>);
       if (pv == 2 || (pv < 0 && kRollDefault))
         return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 2, OCC, true>);
       return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 0, OCC, true>);
