@@ -437,6 +437,7 @@ static const void* pass_fn_mode(int mode, bool panel) {
   X_(V_, 16, 4, 4, 1) X_(V_, 16, 16, 4, 1) X_(V_, 8, 8, 16, 1) X_(V_, 8, 4, 8, 1)            \
   X_(V_, 8, 16, 8, 1) X_(V_, 8, 8, 8, 1) X_(V_, 4, 8, 8, 1) X_(V_, 4, 16, 4, 1)              \
   X_(V_, 8, 32, 4, 1) X_(V_, 16, 8, 8, 2) X_(V_, 16, 16, 16, 1) X_(V_, 8, 8, 16, 2)          \
+  X_(V_, 8, 32, 4, 4)                                                                        \
   X_(V_, 16, 32, 8, 2) X_(V_, 16, 64, 4, 2) X_(V_, 16, 64, 16, 1) X_(V_, 8, 16, 8, 2)
 
 static const void* pass_kernel(const PassCfg& cfg, int mode, bool panel = false) {
