@@ -101,8 +101,9 @@ def test_c5_prenoise_noise_is_oma():
 @pytest.mark.parametrize("var", [1e-2, None])
 def test_c5_aircomp_gm_full_batch(var):
     """256 problems of K=50 x d=100k in ProblemPanels through the AirComp gm with Philox
-    draws (10 iterations: gm never meets tol, and the oracle's CPU cost is per
-    iteration); sampled problems vs oracle.gm fed the same draws.
+    draws (at most 10 iterations: with noise gm never meets tol, and the oracle's CPU
+    cost is per iteration; without noise it converges in 4-5); sampled problems vs
+    oracle.gm fed the same draws, iterations +-1.
 
     Bar: rel L2 <= 1e-5 against the fp32 oracle, OR at least as close to the same
     iteration in fp64 (the oracle run on float64 X / guess with the same draws) as the
@@ -120,7 +121,8 @@ def test_c5_aircomp_gm_full_batch(var):
     out, res = gm_batched(Pn, {"maxiter": it, "tol": 1e-5, "guess": g0, "noise_var": var,
                                "seed": seed})
     torch.cuda.synchronize()
-    assert [r.iters for r in res] == [it] * P
+    if var is not None:
+        assert [r.iters for r in res] == [it] * P        # noisy gm never meets tol
     for p in (0, 1, 2, P // 2, P - 2, P - 1):
         runs = []
         for dt in (torch.float32, torch.float64):
@@ -130,7 +132,7 @@ def test_c5_aircomp_gm_full_batch(var):
             ref, tr = orc.gm(X[p].cpu().to(dt), {"maxiter": it, "tol": 1e-5, "noise_var": var,
                                                  "P_max": 1, "guess": g0[p].cpu().to(dt)},
                              draw=draw)
-            assert tr.iters == it
+            assert abs(res[p].iters - tr.iters) <= 1, (p, res[p].iters, tr.iters)
             runs.append(ref.numpy())
         want32, want64 = runs
         got = out[p].cpu().numpy()

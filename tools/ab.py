@@ -1,17 +1,17 @@
 """Interleaved A/B of bench.py under environment variants, on one GPU box.
 
-    python tools/ab.py --rounds 3 --bench "--workload c5 --no-cpu --alt-steps 0" \
+    python tools/ab.py --rounds 3 --bench=--workload,c5,--no-cpu,--alt-steps,0 \
         --variant base= --variant roll=GMAGG_PASS_VARIANT=2 [--out gpurun_out/x/ab.jsonl]
 
 Each round runs every variant once (a fresh bench.py process each, in variant order), so
 box drift hits every variant alike (cdna_hip_programming.md §5.4 rule 24).  Prints one
 JSON line per run and a per-variant summary (median / min / max of the bench value and of
-the dominant kernel's average launch time).  A variant is NAME=[VAR=VALUE[,VAR=VALUE...]].
+the dominant kernel's average launch time).  A variant is NAME=[VAR=VALUE[;VAR=VALUE...]];
+--bench is bench.py's arguments separated by commas (no shell quoting needed).
 """
 import argparse
 import json
 import os
-import shlex
 import statistics
 import subprocess
 import sys
@@ -31,7 +31,7 @@ def main():
     for v in a.variant or ["base="]:
         name, _, envs = v.partition("=")
         env = {}
-        for kv in filter(None, envs.split(",")):
+        for kv in filter(None, envs.split(";")):
             k, _, val = kv.partition("=")
             env[k] = val
         variants.append((name, env))
@@ -40,7 +40,7 @@ def main():
     for r in range(a.rounds):
         for name, env in variants:
             e = dict(os.environ, **env)
-            cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + shlex.split(a.bench)
+            cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + [x for x in a.bench.split(",") if x]
             p = subprocess.run(cmd, env=e, capture_output=True, text=True, timeout=a.timeout)
             if p.returncode != 0:
                 sys.stderr.write(p.stderr[-3000:])
