@@ -11,7 +11,7 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("GMAGG_LIB", os.path.join(HERE, "libgmagg.so"))
+LIB_PATH = os.environ.get("GMAGG_LIB") or os.path.join(HERE, "libgmagg.so")
 ABI_VERSION = 3
 
 GM_MODE_IDEAL, GM_MODE_AIRCOMP = 0, 1
