@@ -631,13 +631,16 @@ __device__ __forceinline__ void h16_step(const _Float16* Lh, const _Float16* Lm,
   h16_step_b<KT, W, KT - 1>(Lh, Lm, off, haw, maw, hao, mao, acc);
 }
 
-// The same tiles on v_mfma_f32_16x16x32_f16 (GMK_H16_SHAPE == 16; A/B builds): each
-// 32 x 32 tile as 2 x 2 sub-tiles of 16 x 16, one 32-column k-step per MFMA.  The same
-// cycles per FLOP as 32x32x16; the chip holds a higher clock on the 16x16 shape under
-// load (MI355X_MICROARCH.md 'DVFS give-back' item 7).  Fragment of rows R0..R0+15,
-// k-step columns c..c+31: lane l holds row R0 + (l & 15), columns c + 8 (l >> 4) .. +7.
+// The same tiles on v_mfma_f32_16x16x32_f16 (GMK_H16_SHAPE == 16, the default since
+// round 3; 32 = the 32x32x16 consumer above): each 32 x 32 tile as 2 x 2 sub-tiles of
+// 16 x 16, one 32-column k-step per MFMA.  The same cycles per FLOP as 32x32x16; the chip
+// holds a higher clock on the 16x16 shape under load (MI355X_MICROARCH.md 'DVFS
+// give-back' item 7): C4 shard Gram partial 2,976 -> 2,916 us, aggregation 171.3 -> 174.5
+// per s, three interleaved rounds on one box (profiles/r3_gram_shape_ab.jsonl).
+// Fragment of rows R0..R0+15, k-step columns c..c+31: lane l holds row R0 + (l & 15),
+// columns c + 8 (l >> 4) .. +7.
 #ifndef GMK_H16_SHAPE
-#define GMK_H16_SHAPE 32
+#define GMK_H16_SHAPE 16
 #endif
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
