@@ -383,51 +383,11 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
   }
 }
 
+// The selection of one staged K x C tile (columns j0 .. j0 + C - 1).
 template <int R, int C, int NWV>
-__global__ void __launch_bounds__(NWV * 64) col_select(const float* __restrict__ X, int64_t K,
-                                                  int64_t d, int64_t ldx, int ws, int mode,
-                                                  int64_t b, int vec4, float* __restrict__ out) {
-  __shared__ float tile[64 * R][C + 1];
-  const int64_t ntiles = (d + C - 1) / C;
-  // XCD-aware: blocks bid and bid+8 run on the same XCD; give them adjacent tiles
-  // so the two halves of a 128-B line (C = 16) are fetched into one L2.
-  int64_t t = blockIdx.x;
-  if (C < 32 && t < ntiles / 16 * 16) t = t / 16 * 16 + (t % 8) * 2 + (t / 8) % 2;
-  const int64_t j0 = t * C;
-  {
-    // float4 per lane (LPR lanes per row segment), 16 loads in flight per thread
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    constexpr int LPR = C / 4, RPI = NWV * 64 / LPR;
-    const int tq = threadIdx.x % LPR, tr = threadIdx.x / LPR;
-    const int64_t col = j0 + 4 * tq;
-    const bool vec = vec4 && col + 4 <= d;
-    for (int64_t base = tr; base < K; base += 16 * RPI) {
-      f4 buf[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int64_t k = base + (int64_t)u * RPI;
-        buf[u] = f4{0.f, 0.f, 0.f, 0.f};
-        if (k < K) {
-          const float* src = elem(X, ldx, ws, k, col);
-          if (vec) {
-            buf[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src));
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) buf[u][e] = col + e < d ? src[e] : 0.f;
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int64_t k = base + (int64_t)u * RPI;
-        if (k < K) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) tile[k][4 * tq + e] = buf[u][e];
-        }
-      }
-    }
-  }
-  __syncthreads();
+__device__ __forceinline__ void select_tile(float (&tile)[64 * R][C + 1], int64_t K, int64_t d,
+                                            int64_t j0, int mode, int64_t b,
+                                            float* __restrict__ out) {
   // wave w selects columns in pairs (w + 2m NWV, w + 2m NWV + NWV): C % (2 NWV) == 0
   static_assert(C % (2 * NWV) == 0, "column pairs");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -494,6 +454,67 @@ __global__ void __launch_bounds__(NWV * 64) col_select(const float* __restrict__
   }
 }
 
+// PERSIST: one grid of co-resident blocks walks the tiles (grid stride), each block
+// loading tile t + grid into registers while its waves select tile t's columns, so the
+// loads of a CU are in flight during its selection instead of only between tiles (the
+// plain form: one tile per block, loads then selection).
+template <int R, int C, int NWV, bool PERSIST>
+__global__ void __launch_bounds__(NWV * 64) col_select(const float* __restrict__ X, int64_t K,
+                                                  int64_t d, int64_t ldx, int ws, int mode,
+                                                  int64_t b, int vec4, float* __restrict__ out) {
+  __shared__ float tile[64 * R][C + 1];
+  const int64_t ntiles = (d + C - 1) / C;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int LPR = C / 4, RPI = NWV * 64 / LPR;
+  static_assert(16 * RPI >= 64 * R, "one round of 16 loads per thread covers the tile");
+  const int tq = threadIdx.x % LPR, tr = threadIdx.x / LPR;
+  // XCD-aware: blocks bid and bid+8 run on the same XCD; give them adjacent tiles
+  // so the two halves of a 128-B line (C = 16) are fetched into one L2.
+  auto tile_of = [&](int64_t v) {
+    return (C < 32 && v < ntiles / 16 * 16) ? v / 16 * 16 + (v % 8) * 2 + (v / 8) % 2 : v;
+  };
+  // float4 per lane (LPR lanes per row segment), 16 loads in flight per thread
+  f4 buf[16];
+  auto load = [&](int64_t t) {
+    const int64_t col = t * C + 4 * tq;
+    const bool vec = vec4 && col + 4 <= d;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int64_t k = tr + (int64_t)u * RPI;
+      buf[u] = f4{0.f, 0.f, 0.f, 0.f};
+      if (k < K) {
+        const float* src = elem(X, ldx, ws, k, col);
+        if (vec) {
+          buf[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) buf[u][e] = col + e < d ? src[e] : 0.f;
+        }
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int64_t k = tr + (int64_t)u * RPI;
+      if (k < K) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tile[k][4 * tq + e] = buf[u][e];
+      }
+    }
+  };
+  int64_t v = blockIdx.x;
+  if (v >= ntiles) return;
+  load(tile_of(v));
+  for (; v < ntiles; v += PERSIST ? (int64_t)gridDim.x : ntiles) {
+    const int64_t j0 = tile_of(v) * C;
+    if (PERSIST) __syncthreads();          // the previous tile's columns are in registers
+    store();
+    __syncthreads();
+    if (PERSIST && v + gridDim.x < ntiles) load(tile_of(v + gridDim.x));
+    select_tile<R, C, NWV>(tile, K, d, j0, mode, b, out);
+  }
+}
 // Krum, step 1: squared distances of every row pair, register-tiled.
 // A block owns a 128 x 128 tile of pairs (row tiles bi <= bj: D is symmetric)
 // over one slice of the columns; each of 512 threads an 8 x 4 sub-tile (8 x 8 with
@@ -690,9 +711,33 @@ hipError_t launch_col_mean(const float* X, int64_t K, int64_t d, int64_t ldx, fl
 hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, int mode,
                              int64_t b, float* out, hipStream_t s, int ws) {
   const int vec4 = reinterpret_cast<uintptr_t>(X) % 16 == 0 && ldx % 4 == 0;
-#define GMK_SEL(R, C, NWV)                                                                    \
-  hipLaunchKernelGGL((col_select<R, C, NWV>), dim3((unsigned)((d + C - 1) / C)), dim3(NWV * 64), 0, \
-                     s, X, K, d, ldx, ws, mode, b, vec4, out)
+  static const int persist = [] {
+    const char* e = getenv("GMAGG_SELECT_PERSIST");
+    return e ? atoi(e) : 1;
+  }();
+  // persistent: as many blocks as are co-resident (at most one per tile)
+  auto resident = [&](const void* fn, int threads) -> unsigned {
+    int dev = 0, cus = 256, occ = 1;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, threads, 0) != hipSuccess || occ < 1)
+      occ = 1;
+    return (unsigned)(cus * occ);
+  };
+#define GMK_SEL(R, C, NWV)                                                                      \
+  do {                                                                                          \
+    const int64_t nt_ = (d + C - 1) / C;                                                        \
+    if (persist) {                                                                              \
+      const unsigned g_ = resident(reinterpret_cast<const void*>(&col_select<R, C, NWV, true>),   \
+                                   NWV * 64);                                                   \
+      hipLaunchKernelGGL((col_select<R, C, NWV, true>), dim3((unsigned)std::min<int64_t>(nt_, g_)), \
+                         dim3(NWV * 64), 0, s, X, K, d, ldx, ws, mode, b, vec4, out);            \
+    } else {                                                                                    \
+      hipLaunchKernelGGL((col_select<R, C, NWV, false>), dim3((unsigned)nt_), dim3(NWV * 64), 0, \
+                         s, X, K, d, ldx, ws, mode, b, vec4, out);                              \
+    }                                                                                           \
+  } while (0)
   // K <= 1024: 8 waves per 69.6-KB tile (one column pair each) so that the CU holds
   // 4 waves per SIMD (the LDS allows 2 tiles) instead of 2
   if (K <= 64) GMK_SEL(1, 32, 4);
