@@ -112,3 +112,31 @@ def test_sharded_decomposition_matches_reference_gm2():
         got[lo:hi] = g
         assert abs(iters - tr.iters) <= 1
     assert float((got - want).norm() / want.norm()) <= 1e-5
+
+
+def _bad_shard_case(rank, world):
+    """A custom shard plan that one rank's library call would refuse (rank 0 ends at a
+    column that is not a multiple of 4): ShardedGM validates every rank's shard
+    collectively, so EVERY rank raises at construction, before any collective of the
+    aggregation (no rank is left waiting in an all-reduce)."""
+    from byzantine_aircomp_amd.sharded import ShardedGM
+    shard = (0, 1001) if rank == 0 else (1024, 2000)
+    try:
+        ShardedGM(2000, device=torch.device("cuda", 0), shard=shard)
+    except ValueError as e:
+        return str(e)
+    return None
+
+
+def test_sharded_bad_shard_raises_on_every_rank():
+    res = run_world(_bad_shard_case)
+    assert all(r is not None and "hi % 4" in r for r in res)
+
+
+def test_shard_alignment_rule():
+    from byzantine_aircomp_amd.sharded import _aligned
+    assert _aligned([(0, 1024), (1024, 2000)], 2000)
+    assert _aligned([(256, 512)], 4096)                 # a rehearsal of one rank's shard
+    assert not _aligned([(0, 1001)], 2000)              # hi not a multiple of 4
+    assert not _aligned([(100, 512)], 2000)             # lo not 256-aligned
+    assert _aligned([(0, 1001)], 1001)                  # ragged end of the update
