@@ -642,6 +642,9 @@ __device__ __forceinline__ void h16_step(const _Float16* Lh, const _Float16* Lm,
 #ifndef GMK_H16_SHAPE
 #define GMK_H16_SHAPE 16
 #endif
+#ifndef GMK_H16_REUSE
+#define GMK_H16_REUSE 1       // own row tiles' fragments reused as column fragments (0: A/B)
+#endif
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 template <int KT, int W, int B>
@@ -651,11 +654,23 @@ __device__ __forceinline__ void h16s_step_b(const _Float16* Lh, const _Float16* 
                                             f32x4v (&acc)[GramShape<KT>::PER_WAVE][4]) {
   if constexpr (B >= W) {
     using O = H16Order<KT, W>;
+    // G = Y Y^T: a B (column) fragment is addressed like the A (row) fragment of the same
+    // rows, so the wave's own row tiles (B == W, B == KT-1-W) reuse their registers: 8 of
+    // the 40 LDS fragment reads of wave 0's k-step (KT = 8) are not issued
     f16x8 hb[2], mb[2];
+    constexpr int AO = KT == 1 ? 0 : KT - 1 - W;
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb) {
-      hb[sb] = *reinterpret_cast<const f16x8*>(Lh + (B * 32 + 16 * sb) * kH16LS + off);
-      mb[sb] = *reinterpret_cast<const f16x8*>(Lm + (B * 32 + 16 * sb) * kH16LS + off);
+      if constexpr (GMK_H16_REUSE && B == W) {
+        hb[sb] = ha[sb];
+        mb[sb] = ma[sb];
+      } else if constexpr (GMK_H16_REUSE && B == AO) {
+        hb[sb] = ho[sb];
+        mb[sb] = mo[sb];
+      } else {
+        hb[sb] = *reinterpret_cast<const f16x8*>(Lh + (B * 32 + 16 * sb) * kH16LS + off);
+        mb[sb] = *reinterpret_cast<const f16x8*>(Lm + (B * 32 + 16 * sb) * kH16LS + off);
+      }
     }
     constexpr int tw = O::slot_w(B);
 #pragma unroll
