@@ -16,7 +16,7 @@ import ctypes as C
 import torch
 
 from . import _lib
-from .aggregators import GMResult, _ALGO_NAMES, _seed, _stream_ptr, context
+from .aggregators import GMResult, _ALGOS, _ALGO_NAMES, _seed, _stream_ptr, context
 from .panels import panel_width
 
 __all__ = ["gm2_batched", "gm_batched", "oma_batched", "ProblemPanels", "SEED_STRIDE"]
@@ -120,6 +120,10 @@ def _run(X, options: dict, aircomp: bool):
     o.mode = _lib.GM_MODE_AIRCOMP if aircomp else _lib.GM_MODE_IDEAL
     o.check_every = int(opts.get("check_every", 0))
     o.layout = _lib.GM_LAYOUT_PANELS if panels else _lib.GM_LAYOUT_ROWS
+    # "auto" (problems that fit on chip run register-resident, X read once), "stream"
+    # (one streaming pass per iteration over every problem) or "resident" (raises if the
+    # shape does not fit)
+    o.algo = _ALGOS[opts.get("algo", "auto")]
     if pre_var is not None:
         o.pre_oma = 1
         o.pre_oma_var = float(pre_var)

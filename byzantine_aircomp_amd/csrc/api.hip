@@ -341,6 +341,98 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   return GM_OK;
 }
 
+// Batched problems that fit on chip (resident_batched.hip, BASELINE C5): every problem's
+// X is read once and held in VGPRs (+ LDS) for all its iterations, instead of once per
+// pass.  Returns kRbNotTaken when the shape is not eligible, or when the kernel timed out
+// (blocks not co-resident) before touching X: the caller streams.  GMAGG_BATCH_RESIDENT=0
+// turns it off (A/B).
+constexpr int kRbNotTaken = 1;
+int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_t d,
+                         int64_t ldx, int64_t ldp, bool panels, int64_t Wp, const float* guess0,
+                         int64_t ldg, float* out, int64_t ldo, const gm_opts* o,
+                         gm_result* results, hipStream_t s) {
+  static const bool on = [] {
+    const char* e = getenv("GMAGG_BATCH_RESIDENT");
+    return !(e && atoi(e) == 0);
+  }();
+  if (!on || c->d_total > 0) return kRbNotTaken;
+  if (o->mode == GM_MODE_AIRCOMP && o->noise_source != GM_NOISE_PHILOX) return kRbNotTaken;
+  // float4 tile rows: 16-byte aligned problems, rows and panels
+  if ((reinterpret_cast<uintptr_t>(X) & 15) || ldp % 4 || ldx % 4 || (panels && Wp % 4))
+    return kRbNotTaken;
+  const int64_t pbytes = panels ? (d + Wp - 1) / Wp * ldx * 4 : K * ldx * 4;
+  if (pbytes >= ((int64_t)1 << 31)) return kRbNotTaken;
+  RbPlan plan{};
+  if (!rb_plan(K, d, P, o->mode, c->num_cu, &plan)) return kRbNotTaken;
+
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t r0 = off; off = align_up(off + bytes, 256); return r0; };
+  const size_t o_st = take(sizeof(KState) * P), o_flag = take(16);
+  const size_t o_gran = take(sizeof(unsigned long long) * rb_gran_words(K, plan));
+  if (off > c->ws_bytes) {
+    if (c->ws) HIPCHK(hipFree(c->ws));
+    c->ws = nullptr;
+    c->ws_bytes = 0;
+    HIPCHK(hipMalloc(&c->ws, off));
+    c->ws_bytes = off;
+  }
+  int rc = ensure_host(c, sizeof(KState) * P + 256);
+  if (rc) return rc;
+  char* b = c->ws;
+  KState* st = reinterpret_cast<KState*>(b + o_st);
+  unsigned* flag = reinterpret_cast<unsigned*>(b + o_flag);
+  HIPCHK(hipMemsetAsync(b, 0, off, s));          // states, the timeout word, every tag = 0
+
+  ResBArgs a{};
+  a.X = X; a.P = P; a.K = K; a.d = d; a.ldx = ldx; a.x_ps = ldp;
+  a.pstride = panels ? ldx : 0;
+  int ws = 0;
+  while (panels && ((int64_t)1 << ws) < Wp) ++ws;
+  a.wshift = ws;
+  a.prob_bytes = (int)pbytes;
+  a.nb = plan.nb;
+  a.guess0 = guess0; a.ldg = ldg; a.out = out; a.ldo = ldo;
+  a.maxiter = o->maxiter; a.tol = (float)o->tol; a.eps = (float)o->eps;
+  a.mode = o->mode; a.has_noise = o->mode == GM_MODE_AIRCOMP && o->has_noise;
+  a.P_max = o->P_max; a.noise_sd = std::sqrt(std::max(0.0, o->noise_var) / 2.0);
+  a.seed = o->seed;
+  a.pre_oma = o->pre_oma ? 1 : 0;
+  a.oma_sd = (float)std::sqrt(std::max(0.0, o->pre_oma_var));
+  a.oma_seed = o->pre_oma_seed;
+  a.gran = reinterpret_cast<unsigned long long*>(b + o_gran);
+  a.flag = flag;
+  a.st = st;
+  hipEvent_t e0, e1;
+  rc = record_pass_begin(c, s, &e0, &e1);
+  if (rc) return rc;
+  HIPCHK(launch_resident_batched(plan, a, res_coop_launch(), s));
+  rc = record_pass_end(c, s, e0, e1);
+  if (rc) return rc;
+  KState* hst = reinterpret_cast<KState*>(c->host);
+  unsigned* hflag = reinterpret_cast<unsigned*>(c->host + sizeof(KState) * P);
+  HIPCHK(hipMemcpyAsync(hst, st, sizeof(KState) * P, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hflag, flag, 16, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (hflag[0]) {
+    if (c->timing && !c->ev_used.empty()) {
+      c->ev_free.push_back(c->ev_used.back().first);
+      c->ev_free.push_back(c->ev_used.back().second);
+      c->ev_used.pop_back();
+    }
+    // the blocks were not co-resident long enough; with the fused pre-noise some problems
+    // may already carry their noise, so the call cannot simply be streamed again
+    if (o->pre_oma)
+      return fail(GM_ERR_HIP, "batched resident kernel timed out after the fused pre-noise "
+                  "began (another process sharing the GPU?); X is partly noised");
+    return kRbNotTaken;
+  }
+  if (results)
+    for (int64_t p = 0; p < P; ++p)
+      results[p] = gm_result{hst[p].iters, hst[p].last_movement, hst[p].converged,
+                             GM_ALGO_RESIDENT, GM_GUARD_NONE, 0};
+  return GM_OK;
+}
+
 // Gram-space gm2 (gram.hip): G = X'X'^T once (MFMA), the Weiszfeld loop in K-space
 // (one launch, fp64), one closing pass g = sum_k a_k x_k.  Two reads of X.
 //
@@ -992,6 +1084,16 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   WsOrder order(c, s);
   HIPCHK(order.err);
+  // Problems that fit on chip (K <= 52, d <= ~500k): the register-resident batched kernel
+  // reads each problem's X once (resident_batched.hip); AUTO or GM_ALGO_RESIDENT
+  if (o->maxiter > 0 && (o->algo == GM_ALGO_AUTO || o->algo == GM_ALGO_RESIDENT)) {
+    const int rcr = run_resident_batched(c, X, P, K, d, ldx, ldp, panels, Wp, guess0, ldg, out,
+                                         ldo, o, results, s);
+    if (rcr != kRbNotTaken) return rcr;
+  }
+  if (o->algo == GM_ALGO_RESIDENT)
+    return fail(GM_ERR_UNSUPPORTED, "batched resident kernel: K <= 52 (gm2) / K <= 16 (gm), "
+                "d <= %lld, 16-byte aligned problems", (long long)c->num_cu * 2048);
   // Row-major AirComp problems over >= 64 passes: pack them once into the context's panel
   // buffer and stream every pass from it, as gm_weiszfeld_f32 does (C5 AirComp reading on
   // rows: every problem runs all 1000 iterations).

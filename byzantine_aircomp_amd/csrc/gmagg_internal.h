@@ -124,6 +124,41 @@ struct ResArgs {
 bool resident_plan(const PassCfg& cfg, int64_t nch, int num_cu, int* cpb, int* nb);
 size_t resident_gran_words(int64_t K, const PassCfg& cfg, int nb);
 hipError_t launch_resident(const PassCfg& cfg, int cpb, int grid, const ResArgs& a, hipStream_t s);
+bool res_coop_launch();   // GMAGG_RES_COOP=1: cooperative launches (resident.hip)
+
+// Register-resident batched kernel (resident_batched.hip, C5): NG groups of NB blocks,
+// group g runs problems g, g + NG, ... each held in VGPRs for all its iterations.
+struct ResBArgs {
+  const float* X;         // problem p at X + p * x_ps; rows [K][ldx] or panels (pstride > 0)
+  int64_t P, K, d, ldx, x_ps, pstride;
+  int wshift;             // panels: W = 1 << wshift
+  int prob_bytes;         // bytes of one problem's buffer (< 2^31; the loads' range)
+  int nb;                 // blocks per group
+  const float* guess0;
+  int64_t ldg;
+  float* out;
+  int64_t ldo;
+  int64_t maxiter;
+  float tol, eps;
+  int mode, has_noise;
+  double P_max, noise_sd;
+  uint64_t seed;          // AirComp Philox key (problem p: seed + p * kSeedStride)
+  int pre_oma;            // gm2 --var: OMA pre-noise in registers, written back to X
+  float oma_sd;
+  uint64_t oma_seed;
+  unsigned long long* gran;  // [NG][2][NB][2K + 2] {tag, fp32} granules (zeroed per call)
+  unsigned* flag;         // [0] timeout flag (zeroed per call)
+  KState* st;             // [P]
+};
+struct RbPlan {
+  int kr;                 // rows held per thread (K rounded up: 16, 32 or 52)
+  int nb;                 // blocks per problem (2048 columns each)
+  int ng;                 // problems in flight (groups)
+  int mode;               // gm_mode (the kernel is built per mode)
+};
+bool rb_plan(int64_t K, int64_t d, int64_t P, int mode, int num_cu, RbPlan* plan);
+size_t rb_gran_words(int64_t K, const RbPlan& plan);
+hipError_t launch_resident_batched(const RbPlan& plan, const ResBArgs& a, bool coop, hipStream_t s);
 
 // Gram-space variant (gram.hip).  KT = K padded to 32-row tiles (0: unsupported).
 // H16: scaled f16 h+m split, 3 products on v_mfma_f32_32x32x16_f16 (default);

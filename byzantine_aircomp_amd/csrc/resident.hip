@@ -3,7 +3,7 @@
 // iterations per training step, 96 % of the reference's step time).
 //
 // At that size a launch-per-phase loop is launch-bound (3 kernels + polls per
-// iteration).  Here ONE cooperative launch runs every iteration: each block
+// iteration).  Here ONE launch (every block co-resident) runs every iteration: each block
 // owns CPB consecutive J-column chunks of X, loaded into VGPRs once; per
 // iteration it
 //   1. gathers every block's partials of the previous pass and reduces them in
@@ -604,10 +604,27 @@ size_t resident_gran_words(int64_t K, const PassCfg& cfg, int nb) {
   return (size_t)2 * nb * (size_t)(2 * K + 2);
 }
 
+bool res_coop_launch() {
+  static const bool coop = [] {
+    const char* e = getenv("GMAGG_RES_COOP");
+    return e && atoi(e) != 0;
+  }();
+  return coop;
+}
+
 hipError_t launch_resident(const PassCfg& cfg, int cpb, int grid, const ResArgs& a, hipStream_t s) {
   const void* fn = resident_kernel(cfg, cpb);
   if (!fn) return hipErrorInvalidValue;
   void* args[] = {const_cast<ResArgs*>(&a)};
+  // A plain launch by default: co-residency is established by resident_plan's occupancy
+  // test (and policed by the wall-clock-bounded polls), not by a cooperative launch.  A
+  // process that made a cooperative launch segfaults inside the ROCm runtime's exit
+  // handlers under rocprofv3 --kernel-trace — a 40-line program with none of this library
+  // does too (tools/coop_exit_probe.hip, profiles/r3s2_c2_exit_crash.txt) — and the plain
+  // launch costs nothing (C2 158.4 vs 159.7 aggregations/s, interleaved A/B).
+  // GMAGG_RES_COOP=1: the cooperative launch (A/B).
+  const bool coop = res_coop_launch();
+  if (!coop) return hipLaunchKernel(fn, dim3(grid), dim3(cfg.NW * 64), args, 0, s);
   return hipLaunchCooperativeKernel(fn, dim3(grid), dim3(cfg.NW * 64), args, 0, s);
 }
 

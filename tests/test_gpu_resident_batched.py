@@ -1,0 +1,166 @@
+"""The register-resident batched kernel (resident_batched.hip; row f1, BASELINE C5).
+
+Every problem's X is read once and kept in VGPRs (+ LDS rows at 33 <= K <= 52) for all
+its iterations.  Pinned against the oracle (gm2, M:162-184: rel L2 <= 1e-5, iterations
++-1), against the streaming batched path on the same problems, and, for the fused OMA
+pre-noise (M:351-352 -> M:385-394), bit for bit against the standalone batched OMA.
+"""
+import pytest
+import torch
+
+from conftest import rel_l2
+from oracle import aggregators as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _problems(P, K, d, seed, spread=5e-4):
+    g = torch.Generator().manual_seed(seed)
+    p = 0.07 * torch.randn(P, 1, d, generator=g)
+    X = p + spread * torch.randn(P, K, d, generator=g)
+    for i in range(P):
+        B = (0, 5, 10)[i % 3] if K >= 20 else (0, 1)[i % 2] if K >= 4 else 0
+        if B:
+            X[i, K - B:] = p[i] + 10 * spread * torch.randn(B, d, generator=g) + 2e-3
+    return X, p[:, 0, :]
+
+
+def _to(X, layout):
+    """Panels, or row-major problems whose rows start 16-byte aligned (the resident kernel's
+    float4 rows; a contiguous [P, K, d] tensor with d % 4 != 0 is streamed instead): a
+    [P, K, d] view of a [P, K, d rounded up to 4] tensor."""
+    from byzantine_aircomp_amd.batched import ProblemPanels
+    X = X.cuda()
+    if layout == "panels":
+        return ProblemPanels.from_rows(X)
+    P, K, d = X.shape
+    buf = torch.zeros(P, K, -(-d // 4) * 4, device="cuda")
+    buf[:, :, :d] = X
+    return buf[:, :, :d]
+
+
+# K: every row tile (16 / 32 rows in VGPRs; 52 = 36 in VGPRs + 16 in LDS) and its edges;
+# d: a partial float4 group, one block, block edges, several blocks, C2's and C5's d
+@pytest.mark.parametrize("K,d", [(1, 100), (3, 5), (16, 2048), (17, 2049), (32, 4097),
+                                 (33, 7850), (50, 7851), (50, 100_000), (52, 20_000)])
+@pytest.mark.parametrize("layout", ["rows", "panels"])
+def test_resident_gm2_matches_oracle(K, d, layout):
+    from byzantine_aircomp_amd.batched import gm2_batched
+    P = 3
+    X, p = _problems(P, K, d, seed=K * 1000 + d)
+    out, res = gm2_batched(_to(X, layout), {"maxiter": 1000, "guess": p.cuda(),
+                                            "algo": "resident"})
+    for i in range(P):
+        assert res[i].algo == "resident"
+        want, tr = orc.gm2(X[i].clone(), {"maxiter": 1000, "tol": 1e-5, "guess": p[i].clone()})
+        assert rel_l2(out[i].cpu().numpy(), want.numpy()) <= 1e-5
+        assert abs(res[i].iters - tr.iters) <= 1
+
+
+@pytest.mark.parametrize("layout", ["rows", "panels"])
+def test_resident_many_problems_per_group(layout):
+    """More problems than groups in flight: each group runs several problems back to back
+    (its pass counter and granule buffers carry over); vs the streaming batched path."""
+    from byzantine_aircomp_amd.batched import gm2_batched
+    P, K, d = 37, 50, 60_000
+    X, p = _problems(P, K, d, seed=11)
+    X[5] = torch.randn(K, d)          # a slower problem in the middle of a group's queue
+    # (tol 1e-5: at ||g|| ~ 17 the reference's own fp32 movement has a noise floor of
+    # ~2e-6, so a tol of 1e-6 would pin rounding, not the algorithm)
+    opts = {"maxiter": 1000, "guess": p.cuda(), "tol": 1e-5}
+    out_r, res_r = gm2_batched(_to(X, layout), dict(opts, algo="resident"))
+    out_s, res_s = gm2_batched(_to(X, layout), dict(opts, algo="stream"))
+    assert len({r.iters for r in res_r}) > 1
+    for i in range(P):
+        assert res_r[i].algo == "resident" and res_s[i].algo == "stream"
+        assert rel_l2(out_r[i].cpu().numpy(), out_s[i].cpu().numpy()) <= 1e-5
+        assert abs(res_r[i].iters - res_s[i].iters) <= 1
+    for i in (0, 5, P - 1):
+        want, tr = orc.gm2(X[i].clone(), {"maxiter": 1000, "tol": 1e-5, "guess": p[i].clone()})
+        assert rel_l2(out_r[i].cpu().numpy(), want.numpy()) <= 1e-5
+        assert abs(res_r[i].iters - tr.iters) <= 1
+
+
+@pytest.mark.parametrize("layout", ["rows", "panels"])
+@pytest.mark.parametrize("K,d", [(50, 30_001), (12, 4096)])
+def test_resident_fused_prenoise_is_oma(layout, K, d):
+    """gm2 --var v: the pre-noise applied in registers and written back equals the
+    standalone batched OMA bit for bit; the aggregates match OMA then gm2 (streaming)."""
+    from byzantine_aircomp_amd.batched import ProblemPanels, gm2_batched, oma_batched
+    P = 9
+    X, p = _problems(P, K, d, seed=3 + K)
+    A, B = _to(X, layout), _to(X, layout)
+    opts = {"maxiter": 1000, "guess": p.cuda()}
+    out_r, res_r = gm2_batched(A, dict(opts, algo="resident", pre_oma_var=1e-2, pre_oma_seed=77))
+    oma_batched(B, 1e-2, seed=77)
+    out_s, res_s = gm2_batched(B, dict(opts, algo="stream"))
+    ra = A.to_rows() if isinstance(A, ProblemPanels) else A
+    rb = B.to_rows() if isinstance(B, ProblemPanels) else B
+    assert torch.equal(ra, rb)
+    for i in range(P):
+        assert res_r[i].algo == "resident"
+        assert rel_l2(out_r[i].cpu().numpy(), out_s[i].cpu().numpy()) <= 1e-5
+        assert abs(res_r[i].iters - res_s[i].iters) <= 1
+    for i in (0, P - 1):
+        want, tr = orc.gm2(rb[i].cpu().clone(), {"maxiter": 1000, "tol": 1e-5,
+                                                 "guess": p[i].clone()})
+        assert rel_l2(out_r[i].cpu().numpy(), want.numpy()) <= 1e-5
+        assert abs(res_r[i].iters - tr.iters) <= 1
+
+
+def test_resident_strided_rows():
+    """Row-major problems with padded rows (ldx > d) and a problem stride > K * ldx."""
+    from byzantine_aircomp_amd.batched import gm2_batched
+    P, K, d = 4, 40, 10_000
+    X, p = _problems(P, K, d, seed=21)
+    big = torch.zeros(P, K + 3, d + 12, device="cuda")
+    big[:, :K, :d] = X.cuda()
+    view = big[:, :K, :d]
+    assert view.stride(1) == d + 12 and view.stride(0) == (K + 3) * (d + 12)
+    out, res = gm2_batched(view, {"maxiter": 1000, "guess": p.cuda(), "algo": "resident"})
+    for i in range(P):
+        assert res[i].algo == "resident"
+        want, tr = orc.gm2(X[i].clone(), {"maxiter": 1000, "tol": 1e-5, "guess": p[i].clone()})
+        assert rel_l2(out[i].cpu().numpy(), want.numpy()) <= 1e-5
+        assert abs(res[i].iters - tr.iters) <= 1
+
+
+def test_resident_aircomp_vs_stream():
+    """AirComp gm (K <= 16 runs resident): the same Philox draws as the streaming path,
+    so the two agree to rounding over a fixed number of iterations."""
+    from byzantine_aircomp_amd.batched import gm_batched
+    P, K, d = 5, 12, 9000
+    X, p = _problems(P, K, d, seed=4)
+    X, p = X.cuda(), p.cuda()
+    opts = {"maxiter": 25, "tol": 1e-5, "noise_var": 1e-2, "seed": 5, "guess": p}
+    out_r, res_r = gm_batched(X, dict(opts, algo="resident"))
+    out_s, res_s = gm_batched(X, dict(opts, algo="stream"))
+    for i in range(P):
+        assert res_r[i].algo == "resident" and res_r[i].iters == 25
+        assert rel_l2(out_r[i].cpu().numpy(), out_s[i].cpu().numpy()) <= 1e-4
+
+
+def test_resident_unsupported_shape_raises():
+    from byzantine_aircomp_amd.batched import gm2_batched
+    X, p = _problems(2, 60, 1000, seed=1)         # K > 52: no resident tile
+    with pytest.raises(RuntimeError):
+        gm2_batched(X.cuda(), {"maxiter": 100, "guess": p.cuda(), "algo": "resident"})
+    out, res = gm2_batched(X.cuda(), {"maxiter": 100, "guess": p.cuda()})   # AUTO streams
+    assert res[0].algo == "stream"
+    X, p = _problems(2, 10, 1001, seed=2)         # rows not 16-byte aligned (d % 4 != 0)
+    out, res = gm2_batched(X.cuda(), {"maxiter": 100, "guess": p.cuda()})
+    assert res[0].algo == "stream"
+    want, tr = orc.gm2(X[0].clone(), {"maxiter": 100, "tol": 1e-5, "guess": p[0].clone()})
+    assert rel_l2(out[0].cpu().numpy(), want.numpy()) <= 1e-5
+
+
+def test_resident_maxiter_zero_and_one():
+    from byzantine_aircomp_amd.batched import gm2_batched
+    X, p = _problems(3, 20, 3000, seed=9)
+    out, res = gm2_batched(X.cuda(), {"maxiter": 0, "guess": p.cuda()})
+    assert torch.equal(out.cpu(), p)
+    out, res = gm2_batched(X.cuda(), {"maxiter": 1, "guess": p.cuda(), "algo": "resident"})
+    for i in range(3):
+        want, tr = orc.gm2(X[i].clone(), {"maxiter": 1, "tol": 1e-5, "guess": p[i].clone()})
+        assert res[i].iters == 1 == tr.iters
+        assert rel_l2(out[i].cpu().numpy(), want.numpy()) <= 1e-5
