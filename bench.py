@@ -371,7 +371,52 @@ def run_c5(args, json_out, rank=0, world=1):
                "groups": {str(k): {"problems_per_s": v["problems"] / v["seconds"],
                                    "mean_iters": v["iters"] / v["problems"]}
                           for k, v in a_groups.items()}}
-    traffic, traffic_src = pmc_traffic("c5", "panels" if use_panels else "rows")
+    algo_used = outs[(groups[0][0], groups[0][2])][1][0].algo
+    if algo_used == "resident":
+        # the register-resident batched kernel reads each problem's X once (and, in the
+        # prenoise reading, writes the noised copy back once): price THOSE bytes; the
+        # iterations run on chip, so the kernel is bound by the exchange latency per
+        # iteration, and `streaming_equivalent` is the streaming algorithm's bytes over
+        # the same time (it exceeds the HBM peak when the residency pays)
+        hbm_bytes = sum(((2 if (args.reading == "prenoise" and var > 0) else 1)
+                         * g0.shape[0] * 4.0 * K * d) for _, var, _, _, g0, _ in groups)
+        per_launch = hbm_bytes / max(launches / max(args.steps, 1), 1)
+        traffic, traffic_src = pmc_traffic("c5", "panels" if use_panels else "rows",
+                                           kernel="weiszfeld_resident_batched")
+        achieved = hbm_bytes * args.steps / (pass_ms / 1e3) / 1e9 if pass_ms > 0 else None
+        roofline = {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+            "traffic_unit": "GB per launch (one 1024-problem group, PMC)",
+            "traffic_algorithmic": per_launch / 1e9, "traffic_source": traffic_src,
+            "kernel": "weiszfeld_resident_batched (each problem's X read once, held in VGPRs + "
+                      "LDS for all its iterations)",
+            "launches_timed": launches, "avg_launch_us": 1e3 * pass_ms / max(launches, 1),
+            "algorithmic_bytes": "4*K*d per problem (one read of X) + 4*K*d per problem of the "
+                                 "prenoise groups (the noised X written back), / summed kernel time",
+            "streaming_equivalent_GBs": step_bytes * args.steps / (pass_ms / 1e3) / 1e9
+            if pass_ms > 0 else None,
+            "streaming_equivalent_def": "sum_p 4*K*d*iters_p (the streaming path's STEP-pass "
+                                        "bytes) / summed kernel time",
+            "aggregation_frac": agg_bytes / (total / args.steps) / 1e9 / HBM_PEAK_GBS,
+            "aggregation_frac_def": "sum_p 4*K*d*(iters_p+1) / ms_per_step / 8 TB/s: the "
+                                    "streaming algorithm's bytes over the sweep's time"}
+    else:
+        traffic, traffic_src = pmc_traffic("c5", "panels" if use_panels else "rows")
+        roofline = {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+            "traffic_unit": "GB per batched STEP launch with every problem of a "
+                            f"{chunk}-problem group active (PMC of the AirComp reading)",
+            "traffic_algorithmic": chunk * 4.0 * K * d / 1e9 if traffic else None,
+            "traffic_source": traffic_src,
+            "kernel": "weiszfeld_pass (batched STEP, blockIdx.y = problem)",
+            "launches_timed": launches, "avg_launch_us": 1e3 * pass_ms / max(launches, 1),
+            "algorithmic_bytes": "4*K*d per problem per Weiszfeld iteration (sum over "
+                                 "problems of iters) / summed STEP launch time",
+            "aggregation_frac": agg_bytes / (total / args.steps) / 1e9 / HBM_PEAK_GBS,
+            "aggregation_frac_def": "sum_p 4*K*d*(iters_p+1) / ms_per_step / 8 TB/s "
+                                    "(OMA pre-noise time included, its bytes not)"}
     cpu = None
     if not args.no_cpu and world == 1:
         vi0, _, c00, X0, g00, _ = groups[0]
@@ -395,26 +440,17 @@ def run_c5(args, json_out, rank=0, world=1):
                                    "into gm2's first pass)")
                                   if args.reading == "prenoise" else " (AirComp gm for var > 0)"),
                    "K": K, "d": d, "problems": n_prob, "mean_iters": mean_it, "batch": chunk,
-                   "parallelism": "batched (one launch per pass covers every problem of a group)"
+                   "algo": algo_used,
+                   "parallelism": ("register-resident batched (one launch per group: each problem "
+                                   "held on chip for all its iterations)" if algo_used == "resident"
+                                   else "batched (one launch per pass covers every problem of a group)")
                                   + (f"; problems sharded over {world} GPUs (each rank its own "
                                      f"{n_prob}; no data-path collective)" if world > 1 else ""),
                    "layout": "panels (ProblemPanels)" if use_panels else "rows",
                    "groups": {str(k): {"problems_per_s": v["problems"] / v["seconds"],
                                        "mean_iters": v["iters"] / v["problems"]}
                               for k, v in per_group.items()}},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
-                     "traffic_unit": "GB per batched STEP launch with every problem of a "
-                                     f"{chunk}-problem group active (PMC of the AirComp reading)",
-                     "traffic_algorithmic": chunk * 4.0 * K * d / 1e9 if traffic else None,
-                     "traffic_source": traffic_src,
-                     "kernel": "weiszfeld_pass (batched STEP, blockIdx.y = problem)",
-                     "launches_timed": launches, "avg_launch_us": 1e3 * pass_ms / max(launches, 1),
-                     "algorithmic_bytes": "4*K*d per problem per Weiszfeld iteration (sum over "
-                                          "problems of iters) / summed STEP launch time",
-                     "aggregation_frac": agg_bytes / (total / args.steps) / 1e9 / HBM_PEAK_GBS,
-                     "aggregation_frac_def": "sum_p 4*K*d*(iters_p+1) / ms_per_step / 8 TB/s "
-                                             "(OMA pre-noise time included, its bytes not)"},
+        "roofline": roofline,
         "cpu_baseline": cpu,
         "check": dict(check or {}, max_iters=max(iters), min_iters=min(iters)),
         "alt_layout": alt,

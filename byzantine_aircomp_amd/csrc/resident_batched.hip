@@ -36,6 +36,7 @@ namespace gmk {
 namespace {
 
 constexpr int kRbCols = 2048;                    // columns per block
+
 constexpr uint64_t kRbPollTicks = 200000000ull;  // 2 s at the 100 MHz real-time clock
 constexpr int kRbChunk = 8;                      // granules in flight per poll round
 
@@ -82,31 +83,6 @@ __device__ __forceinline__ bool rb_gather(const gu64* g, int64_t bstride, int fi
   return true;
 }
 
-// transpose_reduce<64, R> (device_util.h) with the lane-dependent keep / send choice
-// made on the bits (x ^ ((x ^ y) & m)): written as selects, the compiler turned them
-// into selects of ARRAY INDICES hoisted out of the row blocks, and every use of e[]
-// into a compare / v_cndmask chain over the whole array (1,350 of each per kernel and
-// 180 VGPRs of index tables).  Same results: the bits of one operand are taken whole.
-template <int R>
-__device__ __forceinline__ void rb_transpose(float (&e)[R], int c) {
-  constexpr int STEPS = ilog2<R>::v;
-#pragma unroll
-  for (int step = 0; step < STEPS; ++step) {
-    const int half = R >> (step + 1);
-    const int o = 32 >> step;
-    const unsigned m = (c & o) ? 0xffffffffu : 0u;
-#pragma unroll
-    for (int i = 0; i < half; ++i) {
-      const unsigned lo = __float_as_uint(e[i]), hi = __float_as_uint(e[i + half]);
-      const unsigned x = (lo ^ hi) & m;
-      const float keep = __uint_as_float(lo ^ x), send = __uint_as_float(hi ^ x);
-      e[i] = keep + __shfl_xor(send, o, 64);
-    }
-  }
-#pragma unroll
-  for (int o = 64 / (2 * R); o >= 1; o >>= 1) e[0] += __shfl_xor(e[0], o, 64);
-}
-
 // Compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N).  Every row index
 // of the tile is a constant expression, so the tile is always split into registers (with
 // plain `#pragma unroll` loops the 52-row kernel's tile was left in scratch).
@@ -118,13 +94,111 @@ __device__ __forceinline__ void sfor(F&& f) {
   }
 }
 
+// transpose_reduce<64, R> (device_util.h) on gfx950's cross-lane moves instead of
+// ds_bpermute (an LDS round trip per shuffle, ~70 of them in a chain per 50 rows):
+//   bit 5: v_permlane32_swap of the pair (e[i], e[i + R/2]) IS the halving step (the low
+//          half of the lanes ends with both lanes' e[i], the high half with both lanes'
+//          e[i + R/2]), then one add;
+//   bit 4: v_permlane16_swap likewise (odd 16-lane rows of one register swapped with the
+//          even rows of the other);
+//   bits 3, 2: the keep / send choice on the bits (x ^ ((x ^ y) & m): written as selects,
+//          the compiler turned them into selects of ARRAY INDICES and every use of e[]
+//          into a compare / v_cndmask chain), and the partner's value through DPP
+//          row_mirror (lane c ^ 15) / row_half_mirror (c ^ 7): the partner differs in the
+//          keep bit and shares the bits above it, so each lane still sums disjoint lane
+//          sets; bits 1, 0: DPP quad_perm (c ^ 2, c ^ 1).
+// Lane c ends with row row_of_lane<64, R>(c) summed over the 64 lanes, as transpose_reduce.
+template <int CTRL>
+__device__ __forceinline__ float rb_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int O>
+__device__ __forceinline__ float rb_partner(float v) {   // lane c's partner across bit O
+  if constexpr (O == 8) return rb_dpp<0x140>(v);         // row_mirror: c ^ 15
+  else if constexpr (O == 4) return rb_dpp<0x141>(v);    // row_half_mirror: c ^ 7
+  else if constexpr (O == 2) return rb_dpp<0x4E>(v);     // quad_perm [2,3,0,1]
+  else return rb_dpp<0xB1>(v);                           // quad_perm [1,0,3,2]
+}
+template <int R>
+__device__ __forceinline__ void rb_transpose(float (&e)[R], int c) {
+  constexpr int STEPS = ilog2<R>::v;
+  sfor<0, STEPS>([&](auto step) {
+    constexpr int half = R >> (step + 1);
+    constexpr int o = 32 >> step;
+    if constexpr (o >= 16) {
+      sfor<0, half>([&](auto i) {
+        const auto r = o == 32 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(e[i]),
+                                                                  __float_as_uint(e[i + half]),
+                                                                  false, false)
+                               : __builtin_amdgcn_permlane16_swap(__float_as_uint(e[i]),
+                                                                  __float_as_uint(e[i + half]),
+                                                                  false, false);
+        e[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      });
+    } else {
+      const unsigned m = (c & o) ? 0xffffffffu : 0u;
+      sfor<0, half>([&](auto i) {
+        const unsigned lo = __float_as_uint(e[i]), hi = __float_as_uint(e[i + half]);
+        const unsigned x = (lo ^ hi) & m;
+        e[i] = __uint_as_float(lo ^ x) + rb_partner<o>(__uint_as_float(hi ^ x));
+      });
+    }
+  });
+  // the lane bits below the halving steps: plain butterflies
+  constexpr int O0 = 64 / (2 * R);
+  if constexpr (O0 >= 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(e[0]), __float_as_uint(e[0]),
+                                                    false, false);
+    e[0] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  if constexpr (O0 >= 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(e[0]), __float_as_uint(e[0]),
+                                                    false, false);
+    e[0] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  if constexpr (O0 >= 8) e[0] += rb_partner<8>(e[0]);
+  if constexpr (O0 >= 4) e[0] += rb_partner<4>(e[0]);
+  if constexpr (O0 >= 2) e[0] += rb_partner<2>(e[0]);
+  if constexpr (O0 >= 1) e[0] += rb_partner<1>(e[0]);
+}
+
+// fp64 sum over the wave, every lane the same bits (each butterfly level adds the same two
+// values in both lanes): the cross-lane moves of rb_transpose on both 32-bit halves
+__device__ __forceinline__ double rb_wave_sum(double v) {
+  auto swap_add = [&](auto swap) {
+    const uint64_t b = __double_as_longlong(v);
+    const auto lo = swap((unsigned)b), hi = swap((unsigned)(b >> 32));
+    const double a0 = __longlong_as_double((long long)(((uint64_t)hi[0] << 32) | lo[0]));
+    const double a1 = __longlong_as_double((long long)(((uint64_t)hi[1] << 32) | lo[1]));
+    v = a0 + a1;
+  };
+  swap_add([](unsigned x) { return __builtin_amdgcn_permlane32_swap(x, x, false, false); });
+  swap_add([](unsigned x) { return __builtin_amdgcn_permlane16_swap(x, x, false, false); });
+  auto part = [&](auto ctrl) {
+    const uint64_t b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, ctrl(), 0xf, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), ctrl(), 0xf, 0xf, false);
+    v += __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+  };
+  part([] { return 0x140; });   // row_mirror
+  part([] { return 0x141; });   // row_half_mirror
+  part([] { return 0x4E; });    // quad_perm [2,3,0,1]
+  part([] { return 0xB1; });    // quad_perm [1,0,3,2]
+  return v;
+}
+
 // Rows [K0, K0 + R) of a per-thread row quantity (f(k) over the thread's 4 columns),
 // transpose-reduced over the wave: lane c ends with row K0 + row_of_lane<64, R>(c);
 // the lanes c % (64 / R) == 0 hold distinct rows and store them to srow.
-template <int R, int K0, int KR, class F>
+template <int R, int K0, int KR, int KV, class F>
 __device__ __forceinline__ void rb_rows(F f, float* srow, int lane) {
   float e[R];
-  sfor<0, R>([&](auto i) { e[i] = f(std::integral_constant<int, K0 + i>{}); });
+  sfor<0, R>([&](auto i) {
+    e[i] = f(std::integral_constant<int, K0 + i>{});
+    // rows held in LDS (k >= KV) are read four at a time: the scheduler would issue every
+    // row's ds_read_b128 first, four live registers per row beside the tile
+    if constexpr (K0 + i >= KV && (i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+  });
   rb_transpose<R>(e, lane);
   if ((lane % (64 / R)) == 0) srow[K0 + row_of_lane<64, R>(lane)] = e[0];
   // one row block at a time: interleaving the blocks (the scheduler's choice) holds every
@@ -132,28 +206,34 @@ __device__ __forceinline__ void rb_rows(F f, float* srow, int lane) {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// All KR rows: blocks of 16, then a tail of 8 and / or 4 (KR % 4 == 0).
-template <int KR, int K0 = 0, class F>
+// All KR rows: blocks of 16, then a tail of 8, 4 and / or 2 (KR even).
+template <int KR, int KV, int K0 = 0, class F>
 __device__ __forceinline__ void rb_all_rows(F f, float* srow, int lane) {
   if constexpr (KR - K0 >= 16) {
-    rb_rows<16, K0, KR>(f, srow, lane);
-    rb_all_rows<KR, K0 + 16>(f, srow, lane);
+    rb_rows<16, K0, KR, KV>(f, srow, lane);
+    rb_all_rows<KR, KV, K0 + 16>(f, srow, lane);
   } else if constexpr (KR - K0 >= 8) {
-    rb_rows<8, K0, KR>(f, srow, lane);
-    rb_all_rows<KR, K0 + 8>(f, srow, lane);
+    rb_rows<8, K0, KR, KV>(f, srow, lane);
+    rb_all_rows<KR, KV, K0 + 8>(f, srow, lane);
   } else if constexpr (KR - K0 >= 4) {
-    rb_rows<4, K0, KR>(f, srow, lane);
+    rb_rows<4, K0, KR, KV>(f, srow, lane);
+    rb_all_rows<KR, KV, K0 + 4>(f, srow, lane);
+  } else if constexpr (KR - K0 >= 2) {
+    rb_rows<2, K0, KR, KV>(f, srow, lane);
   }
 }
 
 }  // namespace
 
-template <int KR, int KV, int MODE>
+// DBG (probe builds, -DGMK_RB_DBG_VARIANTS; 0 in the product): phases skipped to price
+// them (tools/rb_probe.py --dbg): 1 phase B rows, 2 the K-space step, 4 phase A, 8 the
+// gather's wait for the tags, 16 the publish
+template <int KR, int KV, int MODE, int DBG = 0>
 __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   // KR rows per column (K rounded up to 4): rows [0, KV) live in the thread's VGPRs, rows
   // [KV, KR) in LDS (s_x, the thread's own 16 bytes per row).  MODE: gm_mode, a template
   // parameter so that the gm2 kernel carries none of the AirComp code's registers.
-  static_assert(KR % 4 == 0 && KV % 4 == 0 && KV <= KR && KR <= 64, "rows per thread");
+  static_assert(KR % 2 == 0 && KV % 4 == 0 && KV <= KR && KR <= 64, "rows per thread");
   constexpr int NT = 512;
   constexpr int NW = NT / 64;
   constexpr int KL = KR - KV;                      // rows held in LDS
@@ -161,16 +241,14 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   typedef unsigned u4v __attribute__((ext_vector_type(4)));
   __shared__ f4 s_x[KL > 0 ? KL : 1][NT];
-  __shared__ float s_coef[KR];
+  __shared__ float s_coef[NW][KR + 2];  // each wave's own copy of the coefficients
   __shared__ float s_osc[KR];
-  __shared__ float s_rows[NW][KR];
+  // row partials and the waves' movement / norm partials, by the parity of the pass they
+  // belong to: a publish reads buffer p & 1 while the next pass's phase B fills the other
+  __shared__ float s_rows[2][NW][KR];
   __shared__ float s_rows2[NW][KR];
-  __shared__ double s_d2[KR];
-  __shared__ double s_r[KR];
-  __shared__ double s_wp[2];
-  __shared__ float s_fin[2][NW];
+  __shared__ float s_fin[2][2][NW];
   __shared__ double s_part[NT];
-  __shared__ float s_anoise;
   __shared__ int s_ok;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -192,7 +270,7 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   const int64_t e0 = a.pstride ? (col0 >> a.wshift) * a.pstride + (col0 & (W - 1)) : col0;
   const uint32_t voff = any ? (uint32_t)(e0 * 4) : 0x80000000u;
   if (tid == 0) s_ok = 1;
-  if (tid < KR) s_coef[tid] = 0.f;
+  if (tid < NW * (KR + 2)) (&s_coef[0][0])[tid] = 0.f;
 
   f4 x[KV > 0 ? KV : 1];   // the tile's register rows: row k of the thread's 4 columns
   float g[4];              // the iterate at those columns
@@ -212,10 +290,11 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   auto publish = [&](bool with_r) {
     gu64* out = gran + ((int64_t)(pc & 1) * NB + bi) * NV;
     const unsigned tag = pc + 1;
+    const int pb = pc & 1;
     if (tid < K) {
       double sm = 0.0;
 #pragma unroll
-      for (int ww = 0; ww < NW; ++ww) sm += (double)s_rows[ww][tid];
+      for (int ww = 0; ww < NW; ++ww) sm += (double)s_rows[pb][ww][tid];
       rb_put(out + tid, tag, (float)sm);
     }
     if (with_r && tid >= 64 && tid < 64 + K) {
@@ -229,8 +308,8 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
       double m = 0.0, gg = 0.0;
 #pragma unroll
       for (int ww = 0; ww < NW; ++ww) {
-        m += (double)s_fin[0][ww];
-        gg += (double)s_fin[1][ww];
+        m += (double)s_fin[pb][0][ww];
+        gg += (double)s_fin[pb][1][ww];
       }
       rb_put(out + 2 * K, tag, (float)m);
       rb_put(out + 2 * K + 1, tag, (float)gg);
@@ -243,20 +322,19 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
       gn += __shfl_xor(gn, o, 64);
     }
     if (lane == 0) {
-      s_fin[0][w] = mv;
-      s_fin[1][w] = gn;
+      s_fin[pc & 1][0][w] = mv;
+      s_fin[pc & 1][1][w] = gn;
     }
   };
-  // the per-row squared distance over the thread's columns, in column order
+  // the per-row squared distance over the thread's columns, on packed pairs (columns
+  // 0/1 and 2/3: v_pk_add + v_pk_mul + v_pk_fma, then one add: 5 instructions per row
+  // instead of 8); the order (t0^2 + t2^2) + (t1^2 + t3^2)
   auto dist_row = [&](auto k) {
     const f4 r = row(k);
-    float sm = 0.f;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const float t = r[v] - g[v];
-      sm = fmaf(t, t, sm);
-    }
-    return sm;
+    const f2 t01 = f2{r[0], r[1]} - f2{g[0], g[1]};
+    const f2 t23 = f2{r[2], r[3]} - f2{g[2], g[3]};
+    const f2 s2 = __builtin_elementwise_fma(t23, t23, t01 * t01);
+    return s2[0] + s2[1];
   };
 
   for (int64_t p = grp; p < a.P; p += NG) {
@@ -328,10 +406,10 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
 
     // ---- INIT (pass pc): D_k to g_0, ||x_k||^2 (gm), ||g_0||^2
     constexpr bool want_r = MODE == 1;
-    __syncthreads();   // s_rows / s_fin of the previous problem's last publish consumed
-    rb_all_rows<KR>(dist_row, &s_rows[w][0], lane);
+    __syncthreads();   // s_rows2 / s_osc of the previous problem consumed
+    rb_all_rows<KR, KV>(dist_row, &s_rows[pc & 1][w][0], lane);
     if constexpr (want_r) {
-      rb_all_rows<KR>([&](auto k) {
+      rb_all_rows<KR, KV>([&](auto k) {
         const f4 r = row(k);
         float sm = 0.f;
 #pragma unroll
@@ -351,55 +429,71 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
     int64_t it = 0;
     double last_mv = NAN;
     int conv = 0;
+    double r_k = 0.0;     // lane k: ||x_k||^2 (gm), from the INIT pass
     for (;; ++it) {
       // (1) gather pass pc: D (+ r at INIT of gm), movement, ||g||^2; G thread groups
-      // each sum every G-th block, then the group sums are added in group order
+      // each sum every G-th block (one round trip), then every wave adds the G group sums
+      // in group order for the values it needs (no second pass through LDS, no barrier)
+      const int nk = (int)((it == 0 && want_r) ? 2 * K : K);
+      const int ncol = nk + 2;
+      const int G = max(1, min(NT / ncol, NB));
       {
         const gu64* in = gran + (int64_t)(pc & 1) * NB * NV;
         const unsigned tag = pc + 1;
-        const int nk = (int)((it == 0 && want_r) ? 2 * K : K);
-        const int ncol = nk + 2;
-        const int G = max(1, min(NT / ncol, NB));
         bool ok = true;
         if (tid < G * ncol) {
           const int gi = tid / ncol, cc = tid - gi * ncol;
           const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
           double sum;
-          if (rb_gather(in + v, NV, gi, G, NB, tag, tmo, sum)) s_part[tid] = sum;
-          else ok = false;
+          if constexpr ((DBG & 8) != 0) {
+            sum = 0.0;
+            for (int bb = gi; bb < NB; bb += G)
+              sum += (double)__uint_as_float((unsigned)(__hip_atomic_load(
+                  in + v + (int64_t)bb * NV, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+                  0xffffffffull));
+            s_part[tid] = sum;
+          } else if (rb_gather(in + v, NV, gi, G, NB, tag, tmo, sum)) {
+            s_part[tid] = sum;
+          } else {
+            ok = false;
+          }
         }
         if (!ok) s_ok = 0;
         __syncthreads();
         if (s_ok == 0) return;                       // timed out: every thread leaves
-        for (int cc = tid; cc < ncol; cc += NT) {
-          double sum = 0.0;
-          for (int gi = 0; gi < G; ++gi) sum += s_part[gi * ncol + cc];
-          if (cc < K) s_d2[cc] = sum;
-          else if (cc < nk) s_r[cc - K] = sum;
-          else s_wp[cc - nk] = sum;
-        }
         ++pc;
-        __syncthreads();
+      }
+      // every wave: the movement / ||g||^2 sums (uniform) and, lane = client, D_k (and r_k
+      // at INIT of gm), each a fixed-order sum of the G group sums
+      const int k = lane;
+      const bool kv = k < K;
+      double mv2 = 0.0, gn2 = 0.0, d2k = 0.0;
+      for (int gi = 0; gi < G; ++gi) {
+        mv2 += s_part[gi * ncol + nk];
+        gn2 += s_part[gi * ncol + nk + 1];
+        if (kv) d2k += s_part[gi * ncol + k];
+      }
+      if (want_r && it == 0 && kv) {
+        r_k = 0.0;
+        for (int gi = 0; gi < G; ++gi) r_k += s_part[gi * ncol + K + k];
       }
       // (2) tol test of the pass that produced g_it (M:180-183)
       if (it >= 1) {
-        const float mv = (float)sqrt(s_wp[0]);
+        const float mv = (float)sqrt(mv2);
         last_mv = (double)mv;
         if (mv <= a.tol) { conv = 1; break; }
       }
       if (it == a.maxiter) break;
-      // (3) coefficients of pass `it`: one wave, lane = client (K <= 64)
-      if (w == 0) {
-        const int k = lane;
-        const bool kv = k < K;
-        const int kk = kv ? k : 0;                   // (s_d2 / s_r hold KR <= 64 entries)
+      // (3) coefficients of pass `it`, in every wave (lane = client, K <= 64) into the
+      // wave's own LDS copy: the waves need no barrier before phase A
+      float an = 0.f;
+      if constexpr ((DBG & 2) == 0) {
         if constexpr (MODE == 0) {
-          const double wk = kv ? 1.0 / (double)clamp_dist(s_d2[kk], a.eps) : 0.0;   // M:178
-          const double Wsum = wave_sum(wk);
-          if (kv) s_coef[k] = (float)(wk / Wsum);                                   // M:179
-          if (lane == 0) s_anoise = 0.f;
+          const double wk = kv ? 1.0 / (double)clamp_dist(d2k, a.eps) : 0.0;   // M:178
+          const double Wsum = rb_wave_sum(wk);
+          if (k < KR) s_coef[w][k] = kv ? (float)(wk / Wsum) : 0.f;           // M:179
         } else {
-          const float s = sqrtf((float)(s_wp[1] / (double)d));      // M:146
+          const float s = sqrtf((float)(gn2 / (double)d));          // M:146
           const float thr = (s * s) * 500.0f;                         // M:152
           double ck = 0.0;
           if (kv) {
@@ -407,42 +501,54 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
             normal4(seed_p, kStreamChannel, (uint64_t)it, (uint64_t)k, n4);
             const float hr = n4[0] * 0.70710678118654752f, hi = n4[1] * 0.70710678118654752f;
             const float h2 = hr * hr + hi * hi;                       // M:403
-            const float dist = clamp_dist(s_d2[kk], a.eps);
-            const float pk = ((float)s_r[kk] + s * s) / (dist * dist * (float)(d + 1)) / h2;   // M:404
+            const float dist = clamp_dist(d2k, a.eps);
+            const float pk = ((float)r_k + s * s) / (dist * dist * (float)(d + 1)) / h2;   // M:404
             const float pup = pk != pk ? pk : fmaxf(pk, thr);          // M:405
             ck = (double)(sqrtf((float)a.P_max / pup) / dist);         // M:407
           }
-          const double Sc = wave_sum(ck);
+          const double Sc = rb_wave_sum(ck);
           const double nd = !a.has_noise ? 0.0
                             : a.noise_sd * (double)normal1(seed_p, kStreamNoise, (uint64_t)it,
                                                            (uint64_t)d);
           const double scale = (double)s / ((double)s * Sc + nd);     // M:153-155
-          if (kv) s_coef[k] = (float)(ck * scale);
-          if (lane == 0) s_anoise = a.has_noise ? (float)(scale * a.noise_sd) : 0.f;
+          if (k < KR) s_coef[w][k] = kv ? (float)(ck * scale) : 0.f;
+          an = a.has_noise ? (float)(scale * a.noise_sd) : 0.f;
         }
       }
-      __syncthreads();
       // (4) phase A: the thread's columns of g' = sum_k c_k x_k (+ the column noise).
       // Packed FMAs on the tile's own register pairs (x.xy, x.zw): left to itself the
       // compiler paired the FMAs across the wrong elements and copied the whole tile into
       // new pairs first (2 x KR more live registers).  v_pk_fma_f32 is one fused FMA per
       // element: the same bits as fmaf.
       f2 ga = {0.f, 0.f}, gb = {0.f, 0.f};
-      sfor<0, KR / 4>([&](auto qq) {
-        constexpr int k4 = 4 * qq;
-        const f4 cw = *reinterpret_cast<const f4*>(&s_coef[k4]);
-        sfor<0, 4>([&](auto u) {
-          const f4 r = row(std::integral_constant<int, k4 + u>{});
-          constexpr int uu = u;
-          const f2 c2 = {cw[uu], cw[uu]};
-          ga = __builtin_elementwise_fma(c2, f2{r[0], r[1]}, ga);
-          gb = __builtin_elementwise_fma(c2, f2{r[2], r[3]}, gb);
+      if constexpr ((DBG & 4) == 0) {
+        sfor<0, KR / 4>([&](auto qq) {
+          constexpr int k4 = 4 * qq;
+          const f4 cw = *reinterpret_cast<const f4*>(&s_coef[w][k4]);
+          sfor<0, 4>([&](auto u) {
+            const f4 r = row(std::integral_constant<int, k4 + u>{});
+            constexpr int uu = u;
+            const f2 c2 = {cw[uu], cw[uu]};
+            ga = __builtin_elementwise_fma(c2, f2{r[0], r[1]}, ga);
+            gb = __builtin_elementwise_fma(c2, f2{r[2], r[3]}, gb);
+          });
+          // (the scheduler would issue every coefficient / LDS-row read first: KR more live
+          // registers; the LDS rows a quad at a time)
+          if constexpr ((k4 & 15) == 12 || k4 + 4 > KV) __builtin_amdgcn_sched_barrier(0);
         });
-        // (the scheduler would issue every coefficient read first: KR more live registers)
-        if constexpr ((k4 & 15) == 12) __builtin_amdgcn_sched_barrier(0);
-      });
+        if constexpr (KR % 4 == 2) {       // the last two rows (KR = 50)
+          constexpr int k2 = KR - 2;
+          const f2 cw = *reinterpret_cast<const f2*>(&s_coef[w][k2]);
+          sfor<0, 2>([&](auto u) {
+            const f4 r = row(std::integral_constant<int, k2 + u>{});
+            constexpr int uu = u;
+            const f2 c2 = {cw[uu], cw[uu]};
+            ga = __builtin_elementwise_fma(c2, f2{r[0], r[1]}, ga);
+            gb = __builtin_elementwise_fma(c2, f2{r[2], r[3]}, gb);
+          });
+        }
+      }
       float mvp = 0.f, gnp = 0.f;
-      const float an = s_anoise;
       const float gnew4[4] = {ga[0], ga[1], gb[0], gb[1]};
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
@@ -458,12 +564,12 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
         }
         g[v] = gv;
       }
-      // (5) phase B: the distances to the new iterate
-      __syncthreads();   // every wave's reads of s_rows / s_fin (publish of the last pass) done
-      rb_all_rows<KR>(dist_row, &s_rows[w][0], lane);
+      // (5) phase B: the distances to the new iterate, into the buffer of pass pc (the
+      // publish of pass pc - 1 reads the other one)
+      if constexpr ((DBG & 1) == 0) rb_all_rows<KR, KV>(dist_row, &s_rows[pc & 1][w][0], lane);
       wave_fin(mvp, gnp);
       __syncthreads();
-      publish(false);
+      if constexpr ((DBG & 16) == 0) publish(false);
     }
 
     // ---- the problem's aggregate and state
@@ -484,16 +590,35 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
 // (rows, rows in VGPRs): K <= 32 wholly in registers; K <= 52 with rows 36..51 in LDS
 // (a 52-row register tile does not fit 256 VGPRs beside the kernel's own ~90)
 static const void* rb_kernel(int kr, int mode) {
-#define GMK_RB(KR_, KV_)                                                                       \
-  if (kr == KR_)                                                                               \
-    return mode == 0 ? reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 0>) \
-                     : reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 1>);
-  GMK_RB(16, 16) GMK_RB(32, 32) GMK_RB(52, 36)
+#ifdef GMK_RB_DBG_VARIANTS
+  static const int dbg = getenv("GMAGG_RB_DBG") ? atoi(getenv("GMAGG_RB_DBG")) : 0;
+  if (kr == 50 && mode == 0) {
+    switch (dbg) {
+      case 1: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 1>);
+      case 2: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 2>);
+      case 4: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 4>);
+      case 8: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 8>);
+      case 16: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 16>);
+      case 31: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 31>);
+      default: break;
+    }
+  }
+#endif
+#define GMK_RB(KR_, KV_, AIRCOMP_)                                                             \
+  if (kr == KR_) {                                                                             \
+    if (mode == 0) return reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 0>); \
+    if constexpr (AIRCOMP_)                                                                    \
+      return reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 1>);          \
+    return nullptr;                                                                            \
+  }
+  // (the AirComp kernel spills beyond 16 rows: built for K <= 16 only.  K <= 50 keeps 32
+  // rows in VGPRs and 18 in LDS (144 KB); K = 51, 52 36 + 16, with a few VGPRs spilled)
+  GMK_RB(16, 16, true) GMK_RB(32, 32, false) GMK_RB(50, 32, false) GMK_RB(52, 36, false)
 #undef GMK_RB
   return nullptr;
 }
 
-int rb_rows_for(int64_t K) { return K <= 16 ? 16 : K <= 32 ? 32 : K <= 52 ? 52 : 0; }
+int rb_rows_for(int64_t K) { return K <= 16 ? 16 : K <= 32 ? 32 : K <= 50 ? 50 : K <= 52 ? 52 : 0; }
 
 bool rb_plan(int64_t K, int64_t d, int64_t P, int mode, int num_cu, RbPlan* plan) {
   const int kr = rb_rows_for(K);
