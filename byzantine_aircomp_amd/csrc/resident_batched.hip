@@ -36,6 +36,9 @@ namespace gmk {
 namespace {
 
 constexpr int kRbCols = 2048;                    // columns per block
+#ifndef GMK_RB_OMA_ROWS
+#define GMK_RB_OMA_ROWS 2
+#endif
 
 constexpr uint64_t kRbPollTicks = 200000000ull;  // 2 s at the 100 MHz real-time clock
 constexpr int kRbChunk = 8;                      // granules in flight per poll round
@@ -361,15 +364,38 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
     };
     auto roff = [&](auto k) { return __builtin_amdgcn_readfirstlane((int)(k * rstride * 4)); };
     if constexpr (KL > 0) __syncthreads();   // s_x of the previous problem fully read
-    sfor<0, KR>([&](auto k) {
-      f4 v = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsrc(k), voff, roff(k), 2));
-      if (!full) {                 // the partial last group: columns >= d are 0
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (col0 + u >= d) v[u] = 0.f;
-      }
-      set_row(k, v);
+    // Every load issued before any is waited for: the LDS rows straight into LDS
+    // (buffer_load ... lds: LDS-DMA, no registers), the register rows into the tile, then
+    // ONE wait.  Columns >= d of a partial last group are zeroed afterwards (selects on the
+    // register rows; the partial thread rewrites its LDS slots).  A branch per row splits
+    // the loads into basic blocks, each ended by vmcnt(0) — the 50 loads of a problem then
+    // run one HBM round trip at a time; staging the LDS rows through registers spills.
+    sfor<KV, KR>([&](auto k) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsrc(k), (__attribute__((address_space(3))) void*)&s_x[k - KV][w * 64], 16, voff,
+          roff(k), 0, 2);
     });
+    sfor<0, KV>([&](auto k) {
+      x[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsrc(k), voff, roff(k), 2));
+    });
+    __builtin_amdgcn_s_waitcnt(0);                   // every load of the tile landed
+    {
+      bool cok[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) cok[u] = col0 + u < d;
+      sfor<0, KV>([&](auto k) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[k][u] = cok[u] ? x[k][u] : 0.f;
+      });
+      if (!full) {
+        sfor<KV, KR>([&](auto k) {
+          f4 v = s_x[k - KV][tid];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = cok[u] ? v[u] : 0.f;
+          s_x[k - KV][tid] = v;
+        });
+      }
+    }
     // ---- OMA pre-noise (M:385-394), the draws of gm_oma_philox_f32 / the fused pass:
     // element (k, j) takes normal j & 3 of the Philox block (row k, j >> 2), scaled by the
     // row's sd / |h_k|; written back in place (the reference's OMA mutates wList).  Rows
@@ -398,7 +424,10 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
                                                   col0 + u < d ? voff + 4 * u : 0x80000000u,
                                                   roff(k), 0);
         }
-        __builtin_amdgcn_sched_barrier(0);   // one row's draws at a time
+        // GMK_RB_OMA_ROWS rows' draws at a time: one Philox chain per row is latency-bound,
+        // every chain at once spills (hoisting the partial-group test out of the row loop
+        // duplicates the loop and spilled 55-90 VGPRs)
+        if constexpr ((k + 1) % GMK_RB_OMA_ROWS == 0) __builtin_amdgcn_sched_barrier(0);
       });
     }
 #pragma unroll
@@ -550,12 +579,22 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
       }
       float mvp = 0.f, gnp = 0.f;
       const float gnew4[4] = {ga[0], ga[1], gb[0], gb[1]};
+      // AirComp: the column noise of pass `it` (M:411), one Philox block per column, one
+      // at a time (four interleaved Philox chains beside the tile spill)
+      float nz[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (MODE == 1) {
+        if (a.has_noise) {
+          sfor<0, 4>([&](auto v) {
+            nz[v] = normal1(seed_p, kStreamNoise, (uint64_t)it, (uint64_t)(col0 + v));
+            __builtin_amdgcn_sched_barrier(0);
+          });
+        }
+      }
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         float gv = gnew4[v];
         if (col0 + v < d) {
-          if (MODE == 1 && a.has_noise)
-            gv = fmaf(an, normal1(seed_p, kStreamNoise, (uint64_t)it, (uint64_t)(col0 + v)), gv);
+          if (MODE == 1 && a.has_noise) gv = fmaf(an, nz[v], gv);
           const float diff = g[v] - gv;
           mvp = fmaf(diff, diff, mvp);
           gnp = fmaf(gv, gv, gnp);
@@ -621,7 +660,10 @@ static const void* rb_kernel(int kr, int mode) {
 int rb_rows_for(int64_t K) { return K <= 16 ? 16 : K <= 32 ? 32 : K <= 50 ? 50 : K <= 52 ? 52 : 0; }
 
 bool rb_plan(int64_t K, int64_t d, int64_t P, int mode, int num_cu, RbPlan* plan) {
-  const int kr = rb_rows_for(K);
+  int kr = rb_rows_for(K);
+  // GMAGG_RB_ROWS=52: the 36 + 16-row tile for K <= 50 too (A/B of the row split)
+  static const int force = getenv("GMAGG_RB_ROWS") ? atoi(getenv("GMAGG_RB_ROWS")) : 0;
+  if (force == 52 && kr == 50) kr = 52;
   // the AirComp kernel (column draws in phase A, Philox channel draws in the K-space wave)
   // spills beyond 16 rows: K > 16 AirComp problems stream
   if (mode != 0 && kr > 16) return false;
