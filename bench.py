@@ -9,7 +9,9 @@ reference's tol test (||g_t - g_{t+1}|| <= 1e-5) fires — on a synthetic
 K=1000 x d=11M fp32 client matrix already resident in HBM (honest rows ~
 N(0, 0.05^2), the last 20% ~ N(0.25, 0.5^2), guess ~ N(0, 0.01^2); generated on
 the device by Philox).  `--workload c2` is BASELINE config C2 (AirComp `gm`,
-var 1e-2, K=50 x d=7850, 1000 iterations); `c4-shard` one GPU's shard of C4.
+var 1e-2, K=50 x d=7850, 1000 iterations); `c4-shard` a standalone K=256 x d=15.6M
+problem (C4's column count per GPU at N = 8; the d-sharded C4 job itself decides the Gram
+guard on the GLOBAL ||g|| and streams); `c4` the whole 128 GB C4 job.
 
 N > 1: d is sharded over the ranks (sharded.ShardedGM: 256-aligned contiguous
 column shards), each Weiszfeld iteration all-reduces a (K+2)-vector of fp64
@@ -45,7 +47,7 @@ WORKLOADS = {
     # name: (K, d, byzantine rows, default aggregator, default noise variance)
     "c3": (1000, 11_000_000, 200, "gm2", None),
     "c3-small": (1000, 1_000_000, 200, "gm2", None),
-    "c4-shard": (256, 15_625_000, 51, "gm2", None),     # one GPU's shard of K=256 x d=125M
+    "c4-shard": (256, 15_625_000, 51, "gm2", None),     # C4's per-GPU column count, standalone
     "c4": (256, 125_000_000, 51, "gm2", None),          # the whole C4 job (d-sharded over N)
     "c5-problem": (50, 100_000, 10, "gm2", None),
     "c2": (50, 7850, 10, "gm", 1e-2),                   # MNIST MLP d, K=50, B=10, AirComp gm
