@@ -1092,7 +1092,7 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
     if (rcr != kRbNotTaken) return rcr;
   }
   if (o->algo == GM_ALGO_RESIDENT)
-    return fail(GM_ERR_UNSUPPORTED, "batched resident kernel: K <= 52 (gm2) / K <= 16 (gm), "
+    return fail(GM_ERR_UNSUPPORTED, "batched resident kernel: K <= 52 (gm2) / K <= 50 (gm), "
                 "d <= %lld, 16-byte aligned problems", (long long)c->num_cu * 2048);
   // Row-major AirComp problems over >= 64 passes: pack them once into the context's panel
   // buffer and stream every pass from it, as gm_weiszfeld_f32 does (C5 AirComp reading on

@@ -400,7 +400,8 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
     // element (k, j) takes normal j & 3 of the Philox block (row k, j >> 2), scaled by the
     // row's sd / |h_k|; written back in place (the reference's OMA mutates wList).  Rows
     // past K: scale 0 (they stay 0) and a zero-record resource (their stores are dropped).
-    if (a.pre_oma) {
+    // (gm2 only: the AirComp kernel carries no OMA code)
+    if (MODE == 0 && a.pre_oma) {
       const uint64_t oseed = a.oma_seed + (uint64_t)p * kSeedStride;
       __syncthreads();   // s_osc of the previous problem fully read
       if (tid < KR) s_osc[tid] = tid < K ? oma_row_scale(oseed, (uint64_t)tid, a.oma_sd) : 0.f;
@@ -438,6 +439,9 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
     __syncthreads();   // s_rows2 / s_osc of the previous problem consumed
     rb_all_rows<KR, KV>(dist_row, &s_rows[pc & 1][w][0], lane);
     if constexpr (want_r) {
+      // (a memory clobber: without it the LDS rows' reads of the pass above are kept live
+      // for this one — 18 float4 beside the tile)
+      asm volatile("" ::: "memory");
       rb_all_rows<KR, KV>([&](auto k) {
         const f4 r = row(k);
         float sm = 0.f;
@@ -650,9 +654,10 @@ static const void* rb_kernel(int kr, int mode) {
       return reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 1>);          \
     return nullptr;                                                                            \
   }
-  // (the AirComp kernel spills beyond 16 rows: built for K <= 16 only.  K <= 50 keeps 32
-  // rows in VGPRs and 18 in LDS (144 KB); K = 51, 52 36 + 16, with a few VGPRs spilled)
-  GMK_RB(16, 16, true) GMK_RB(32, 32, false) GMK_RB(50, 32, false) GMK_RB(52, 36, false)
+  // (K <= 50 keeps 32 rows in VGPRs and 18 in LDS (144 KB); K = 51, 52 36 + 16, with a few
+  // VGPRs spilled.  The AirComp kernel: K <= 50; at 33..50 rows it spills ~90 VGPRs of
+  // loop invariants, ~44 scratch reloads per iteration)
+  GMK_RB(16, 16, true) GMK_RB(32, 32, true) GMK_RB(50, 32, true) GMK_RB(52, 36, false)
 #undef GMK_RB
   return nullptr;
 }
@@ -664,9 +669,9 @@ bool rb_plan(int64_t K, int64_t d, int64_t P, int mode, int num_cu, RbPlan* plan
   // GMAGG_RB_ROWS=52: the 36 + 16-row tile for K <= 50 too (A/B of the row split)
   static const int force = getenv("GMAGG_RB_ROWS") ? atoi(getenv("GMAGG_RB_ROWS")) : 0;
   if (force == 52 && kr == 50) kr = 52;
-  // the AirComp kernel (column draws in phase A, Philox channel draws in the K-space wave)
-  // spills beyond 16 rows: K > 16 AirComp problems stream
-  if (mode != 0 && kr > 16) return false;
+  // the AirComp kernel (column draws in phase A, Philox channel draws in the coefficient
+  // step) is built for K <= 50 (the 52-row tile spills): K = 51, 52 AirComp problems stream
+  if (mode != 0 && kr > 50) return false;
   const void* fn = kr ? rb_kernel(kr, mode) : nullptr;
   if (!fn || d < 1 || P < 1) return false;
   int n = 0;

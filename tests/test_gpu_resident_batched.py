@@ -125,11 +125,12 @@ def test_resident_strided_rows():
         assert abs(res[i].iters - tr.iters) <= 1
 
 
-def test_resident_aircomp_vs_stream():
-    """AirComp gm (K <= 16 runs resident): the same Philox draws as the streaming path,
+@pytest.mark.parametrize("K,d", [(12, 9000), (30, 8192), (50, 20_000)])
+def test_resident_aircomp_vs_stream(K, d):
+    """AirComp gm (K <= 50 runs resident): the same Philox draws as the streaming path,
     so the two agree to rounding over a fixed number of iterations."""
     from byzantine_aircomp_amd.batched import gm_batched
-    P, K, d = 5, 12, 9000
+    P = 5
     X, p = _problems(P, K, d, seed=4)
     X, p = X.cuda(), p.cuda()
     opts = {"maxiter": 25, "tol": 1e-5, "noise_var": 1e-2, "seed": 5, "guess": p}
@@ -164,3 +165,23 @@ def test_resident_maxiter_zero_and_one():
         want, tr = orc.gm2(X[i].clone(), {"maxiter": 1, "tol": 1e-5, "guess": p[i].clone()})
         assert res[i].iters == 1 == tr.iters
         assert rel_l2(out[i].cpu().numpy(), want.numpy()) <= 1e-5
+
+
+@pytest.mark.parametrize("agg", ["gm2", "gm"])
+@pytest.mark.parametrize("K,d", [(50, 7850), (20, 10_001), (8, 4096)])
+def test_resident_rows_and_panels_identical(agg, K, d):
+    """The resident kernel does the same arithmetic in either layout (a thread owns the same
+    columns; only the addresses differ): 16-byte aligned rows and ProblemPanels give
+    bit-identical aggregates and iteration counts."""
+    from byzantine_aircomp_amd.batched import gm2_batched, gm_batched
+    P = 4
+    X, p = _problems(P, K, d, seed=K + d)
+    f = gm2_batched if agg == "gm2" else gm_batched
+    opts = {"maxiter": 1000 if agg == "gm2" else 12, "tol": 1e-5, "guess": p.cuda(),
+            "algo": "resident"}
+    if agg == "gm":
+        opts.update(noise_var=1e-2, seed=3)
+    a, ra = f(_to(X, "rows"), dict(opts))
+    b, rb = f(_to(X, "panels"), dict(opts))
+    assert torch.equal(a, b)
+    assert [r.iters for r in ra] == [r.iters for r in rb]
