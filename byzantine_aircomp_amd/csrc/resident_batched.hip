@@ -72,7 +72,9 @@ __device__ __forceinline__ bool rb_gather(const gu64* g, int64_t bstride, int fi
         }
       }
       if (ok) break;
+#ifndef GMK_RB_NOSLEEP
       __builtin_amdgcn_s_sleep(1);
+#endif
       if (((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t0 > kRbPollTicks) ||
           __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
