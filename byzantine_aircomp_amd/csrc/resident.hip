@@ -193,6 +193,12 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   float gcur = fin ? a.guess0[gj] : 0.f;       // finisher thread: the iterate at column gj
 
   const int i_c = row_of_lane<LPR, R>(c);
+  // row sums over the LPR lanes of a row segment: at LPR = 64 (the C2 tile) on gfx950's
+  // permlane / DPP moves (device_util.h xlane_transpose64, the same lane -> row map)
+  auto row_reduce = [&](float (&e)[R]) {
+    if constexpr (LPR == 64) xlane_transpose64<R>(e, c);
+    else transpose_reduce<LPR, R>(e, c);
+  };
   // publish this block's partials of pass p (granules, tag p + 1, buffer p & 1)
   auto publish = [&](int64_t p, const double* racc, const double* racc2, double mv, double gn) {
     gu64* out = gran + ((p & 1) * nb + blockIdx.x) * NV;
@@ -221,12 +227,9 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   // barrier): fp32 sums over the finisher lanes (as the reference's fp32 norms),
   // only in the waves that hold finisher columns
   auto wave_partials = [&](float mv, float gn) {
-    if (w * 64 < JB) {
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) {
-        mv += __shfl_xor(mv, o, 64);
-        gn += __shfl_xor(gn, o, 64);
-      }
+    if (w * 64 < JB) {   // (permlane / DPP moves, no LDS round trips: device_util.h)
+      mv = xlane_wave_sum_f32(mv);
+      gn = xlane_wave_sum_f32(gn);
     }
     if (lane == 0) {
       s_fin[0][w] = w * 64 < JB ? (double)mv : 0.0;
@@ -259,8 +262,8 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         e[i] = s1;
         e2[i] = s2;
       }
-      transpose_reduce<LPR, R>(e, c);
-      transpose_reduce<LPR, R>(e2, c);
+      row_reduce(e);
+      row_reduce(e2);
 #pragma unroll
       for (int m = 0; m < RPL; ++m) {
         racc[m] += (double)e[m];
@@ -367,7 +370,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         const bool kv = k < K;
         if (a.mode == 0) {
           const double wk = kv ? 1.0 / (double)clamp_dist(s_d2[k], a.eps) : 0.0;
-          const double W = wave_sum(wk);
+          const double W = xlane_wave_sum(wk);
           if (kv) s_coef[k] = (float)(wk / W);
           if (lane == 0) s_anoise = 0.f;
         } else {
@@ -392,7 +395,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
             const float pup = pk != pk ? pk : fmaxf(pk, thr);          // M:405
             ck = (double)(sqrtf((float)a.P_max / pup) / dist);         // M:407
           }
-          const double Sc = wave_sum(ck);
+          const double Sc = xlane_wave_sum(ck);
           const double nd = !a.has_noise ? 0.0
                             : a.noise_sd * (double)(pre_h2 ? s_nd
                                                            : normal1(a.seed, kStreamNoise,
@@ -504,7 +507,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         }
         e[i] = s1;
       }
-      transpose_reduce<LPR, R>(e, c);
+      row_reduce(e);
 #pragma unroll
       for (int m = 0; m < RPL; ++m) racc[m] += (double)e[m];
     }

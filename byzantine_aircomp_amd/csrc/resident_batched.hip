@@ -88,110 +88,6 @@ __device__ __forceinline__ bool rb_gather(const gu64* g, int64_t bstride, int fi
   return true;
 }
 
-// Compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N).  Every row index
-// of the tile is a constant expression, so the tile is always split into registers (with
-// plain `#pragma unroll` loops the 52-row kernel's tile was left in scratch).
-template <int I0, int N, class F>
-__device__ __forceinline__ void sfor(F&& f) {
-  if constexpr (I0 < N) {
-    f(std::integral_constant<int, I0>{});
-    sfor<I0 + 1, N>(f);
-  }
-}
-
-// transpose_reduce<64, R> (device_util.h) on gfx950's cross-lane moves instead of
-// ds_bpermute (an LDS round trip per shuffle, ~70 of them in a chain per 50 rows):
-//   bit 5: v_permlane32_swap of the pair (e[i], e[i + R/2]) IS the halving step (the low
-//          half of the lanes ends with both lanes' e[i], the high half with both lanes'
-//          e[i + R/2]), then one add;
-//   bit 4: v_permlane16_swap likewise (odd 16-lane rows of one register swapped with the
-//          even rows of the other);
-//   bits 3, 2: the keep / send choice on the bits (x ^ ((x ^ y) & m): written as selects,
-//          the compiler turned them into selects of ARRAY INDICES and every use of e[]
-//          into a compare / v_cndmask chain), and the partner's value through DPP
-//          row_mirror (lane c ^ 15) / row_half_mirror (c ^ 7): the partner differs in the
-//          keep bit and shares the bits above it, so each lane still sums disjoint lane
-//          sets; bits 1, 0: DPP quad_perm (c ^ 2, c ^ 1).
-// Lane c ends with row row_of_lane<64, R>(c) summed over the 64 lanes, as transpose_reduce.
-template <int CTRL>
-__device__ __forceinline__ float rb_dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
-}
-template <int O>
-__device__ __forceinline__ float rb_partner(float v) {   // lane c's partner across bit O
-  if constexpr (O == 8) return rb_dpp<0x140>(v);         // row_mirror: c ^ 15
-  else if constexpr (O == 4) return rb_dpp<0x141>(v);    // row_half_mirror: c ^ 7
-  else if constexpr (O == 2) return rb_dpp<0x4E>(v);     // quad_perm [2,3,0,1]
-  else return rb_dpp<0xB1>(v);                           // quad_perm [1,0,3,2]
-}
-template <int R>
-__device__ __forceinline__ void rb_transpose(float (&e)[R], int c) {
-  constexpr int STEPS = ilog2<R>::v;
-  sfor<0, STEPS>([&](auto step) {
-    constexpr int half = R >> (step + 1);
-    constexpr int o = 32 >> step;
-    if constexpr (o >= 16) {
-      sfor<0, half>([&](auto i) {
-        const auto r = o == 32 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(e[i]),
-                                                                  __float_as_uint(e[i + half]),
-                                                                  false, false)
-                               : __builtin_amdgcn_permlane16_swap(__float_as_uint(e[i]),
-                                                                  __float_as_uint(e[i + half]),
-                                                                  false, false);
-        e[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-      });
-    } else {
-      const unsigned m = (c & o) ? 0xffffffffu : 0u;
-      sfor<0, half>([&](auto i) {
-        const unsigned lo = __float_as_uint(e[i]), hi = __float_as_uint(e[i + half]);
-        const unsigned x = (lo ^ hi) & m;
-        e[i] = __uint_as_float(lo ^ x) + rb_partner<o>(__uint_as_float(hi ^ x));
-      });
-    }
-  });
-  // the lane bits below the halving steps: plain butterflies
-  constexpr int O0 = 64 / (2 * R);
-  if constexpr (O0 >= 32) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(e[0]), __float_as_uint(e[0]),
-                                                    false, false);
-    e[0] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
-  if constexpr (O0 >= 16) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(e[0]), __float_as_uint(e[0]),
-                                                    false, false);
-    e[0] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
-  if constexpr (O0 >= 8) e[0] += rb_partner<8>(e[0]);
-  if constexpr (O0 >= 4) e[0] += rb_partner<4>(e[0]);
-  if constexpr (O0 >= 2) e[0] += rb_partner<2>(e[0]);
-  if constexpr (O0 >= 1) e[0] += rb_partner<1>(e[0]);
-}
-
-// fp64 sum over the wave, every lane the same bits (each butterfly level adds the same two
-// values in both lanes): the cross-lane moves of rb_transpose on both 32-bit halves
-__device__ __forceinline__ double rb_wave_sum(double v) {
-  auto swap_add = [&](auto swap) {
-    const uint64_t b = __double_as_longlong(v);
-    const auto lo = swap((unsigned)b), hi = swap((unsigned)(b >> 32));
-    const double a0 = __longlong_as_double((long long)(((uint64_t)hi[0] << 32) | lo[0]));
-    const double a1 = __longlong_as_double((long long)(((uint64_t)hi[1] << 32) | lo[1]));
-    v = a0 + a1;
-  };
-  swap_add([](unsigned x) { return __builtin_amdgcn_permlane32_swap(x, x, false, false); });
-  swap_add([](unsigned x) { return __builtin_amdgcn_permlane16_swap(x, x, false, false); });
-  auto part = [&](auto ctrl) {
-    const uint64_t b = __double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, ctrl(), 0xf, 0xf, false);
-    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), ctrl(), 0xf, 0xf, false);
-    v += __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-  };
-  part([] { return 0x140; });   // row_mirror
-  part([] { return 0x141; });   // row_half_mirror
-  part([] { return 0x4E; });    // quad_perm [2,3,0,1]
-  part([] { return 0xB1; });    // quad_perm [1,0,3,2]
-  return v;
-}
-
 // Rows [K0, K0 + R) of a per-thread row quantity (f(k) over the thread's 4 columns),
 // transpose-reduced over the wave: lane c ends with row K0 + row_of_lane<64, R>(c);
 // the lanes c % (64 / R) == 0 hold distinct rows and store them to srow.
@@ -204,7 +100,7 @@ __device__ __forceinline__ void rb_rows(F f, float* srow, int lane) {
     // row's ds_read_b128 first, four live registers per row beside the tile
     if constexpr (K0 + i >= KV && (i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
   });
-  rb_transpose<R>(e, lane);
+  xlane_transpose64<R>(e, lane);
   if ((lane % (64 / R)) == 0) srow[K0 + row_of_lane<64, R>(lane)] = e[0];
   // one row block at a time: interleaving the blocks (the scheduler's choice) holds every
   // block's e[] at once, KR more live registers beside the tile
@@ -525,7 +421,7 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
       if constexpr ((DBG & 2) == 0) {
         if constexpr (MODE == 0) {
           const double wk = kv ? 1.0 / (double)clamp_dist(d2k, a.eps) : 0.0;   // M:178
-          const double Wsum = rb_wave_sum(wk);
+          const double Wsum = xlane_wave_sum(wk);
           if (k < KR) s_coef[w][k] = kv ? (float)(wk / Wsum) : 0.f;           // M:179
         } else {
           const float s = sqrtf((float)(gn2 / (double)d));          // M:146
@@ -541,7 +437,7 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
             const float pup = pk != pk ? pk : fmaxf(pk, thr);          // M:405
             ck = (double)(sqrtf((float)a.P_max / pup) / dist);         // M:407
           }
-          const double Sc = rb_wave_sum(ck);
+          const double Sc = xlane_wave_sum(ck);
           const double nd = !a.has_noise ? 0.0
                             : a.noise_sd * (double)normal1(seed_p, kStreamNoise, (uint64_t)it,
                                                            (uint64_t)d);
