@@ -36,6 +36,11 @@ namespace gmk {
 namespace {
 
 constexpr int kRbCols = 2048;                    // columns per block
+// GMK_RB_COEF_WAVE0=1: wave 0 alone forms the coefficients (one more block barrier)
+// instead of every wave redundantly (A/B)
+#ifndef GMK_RB_COEF_WAVE0
+#define GMK_RB_COEF_WAVE0 0
+#endif
 #ifndef GMK_RB_OMA_ROWS
 #define GMK_RB_OMA_ROWS 2
 #endif
@@ -150,6 +155,7 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   __shared__ float s_rows2[NW][KR];
   __shared__ float s_fin[2][2][NW];
   __shared__ double s_part[NT];
+  __shared__ float s_an;
   __shared__ int s_ok;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -418,7 +424,8 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
       // (3) coefficients of pass `it`, in every wave (lane = client, K <= 64) into the
       // wave's own LDS copy: the waves need no barrier before phase A
       float an = 0.f;
-      if constexpr ((DBG & 2) == 0) {
+      constexpr int CW = GMK_RB_COEF_WAVE0 ? 0 : -1;   // the coefficient copy phase A reads
+      if ((DBG & 2) == 0 && (!GMK_RB_COEF_WAVE0 || w == 0)) {
         if constexpr (MODE == 0) {
           const double wk = kv ? 1.0 / (double)clamp_dist(d2k, a.eps) : 0.0;   // M:178
           const double Wsum = xlane_wave_sum(wk);
@@ -445,7 +452,13 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
           if (k < KR) s_coef[w][k] = kv ? (float)(ck * scale) : 0.f;
           an = a.has_noise ? (float)(scale * a.noise_sd) : 0.f;
         }
+        if (GMK_RB_COEF_WAVE0 && lane == 0) s_an = an;
       }
+      if constexpr (GMK_RB_COEF_WAVE0) {
+        __syncthreads();
+        an = s_an;
+      }
+      const int cw_row = CW < 0 ? w : CW;
       // (4) phase A: the thread's columns of g' = sum_k c_k x_k (+ the column noise).
       // Packed FMAs on the tile's own register pairs (x.xy, x.zw): left to itself the
       // compiler paired the FMAs across the wrong elements and copied the whole tile into
@@ -455,7 +468,7 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
       if constexpr ((DBG & 4) == 0) {
         sfor<0, KR / 4>([&](auto qq) {
           constexpr int k4 = 4 * qq;
-          const f4 cw = *reinterpret_cast<const f4*>(&s_coef[w][k4]);
+          const f4 cw = *reinterpret_cast<const f4*>(&s_coef[cw_row][k4]);
           sfor<0, 4>([&](auto u) {
             const f4 r = row(std::integral_constant<int, k4 + u>{});
             constexpr int uu = u;
@@ -469,7 +482,7 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
         });
         if constexpr (KR % 4 == 2) {       // the last two rows (KR = 50)
           constexpr int k2 = KR - 2;
-          const f2 cw = *reinterpret_cast<const f2*>(&s_coef[w][k2]);
+          const f2 cw = *reinterpret_cast<const f2*>(&s_coef[cw_row][k2]);
           sfor<0, 2>([&](auto u) {
             const f4 r = row(std::integral_constant<int, k2 + u>{});
             constexpr int uu = u;
