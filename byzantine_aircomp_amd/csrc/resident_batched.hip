@@ -133,7 +133,8 @@ __device__ __forceinline__ void rb_all_rows(F f, float* srow, int lane) {
 
 // DBG (probe builds, -DGMK_RB_DBG_VARIANTS; 0 in the product): phases skipped to price
 // them (tools/rb_probe.py --dbg): 1 phase B rows, 2 the K-space step, 4 phase A, 8 the
-// gather's wait for the tags, 16 the publish
+// gather's wait for the tags, 16 the publish, 32 the tile load, 64 the INIT rows, 128 the
+// LDS rows' loads, 256 the register rows' loads
 template <int KR, int KV, int MODE, int DBG = 0>
 __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   // KR rows per column (K rounded up to 4): rows [0, KV) live in the thread's VGPRs, rows
@@ -274,14 +275,33 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
     // register rows; the partial thread rewrites its LDS slots).  A branch per row splits
     // the loads into basic blocks, each ended by vmcnt(0) — the 50 loads of a problem then
     // run one HBM round trip at a time; staging the LDS rows through registers spills.
-    sfor<KV, KR>([&](auto k) {
+    if constexpr ((DBG & 32) == 0) {
+    if constexpr ((DBG & 128) == 0) sfor<KV, KR>([&](auto k) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rsrc(k), (__attribute__((address_space(3))) void*)&s_x[k - KV][w * 64], 16, voff,
           roff(k), 0, 2);
     });
-    sfor<0, KV>([&](auto k) {
+    if constexpr ((DBG & 256) == 0) sfor<0, KV>([&](auto k) {
       x[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsrc(k), voff, roff(k), 2));
     });
+    } else if (p == grp) {
+      sfor<0, KV>([&](auto k) { x[k] = f4{0.f, 0.f, 0.f, 0.f}; });
+    }
+    // the guess at the thread's columns, in flight with the tile (one buffer resource:
+    // columns past d read 0)
+    {
+      const uint64_t gb = reinterpret_cast<uint64_t>(a.guess0 + p * a.ldg);
+      float* const Gu = reinterpret_cast<float*>(
+          ((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(gb >> 32)) << 32) |
+          (uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)gb));
+      const __amdgpu_buffer_rsrc_t rg =
+          __builtin_amdgcn_make_buffer_rsrc(Gu, 0, (int)(d * 4), 0x00020000);
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        g[v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                             rg, any ? (uint32_t)((col0 + v) * 4) : 0x80000000u,
+                                             0, 0));
+    }
     __builtin_amdgcn_s_waitcnt(0);                   // every load of the tile landed
     {
       bool cok[4];
@@ -335,13 +355,11 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
         if constexpr ((k + 1) % GMK_RB_OMA_ROWS == 0) __builtin_amdgcn_sched_barrier(0);
       });
     }
-#pragma unroll
-    for (int v = 0; v < 4; ++v) g[v] = col0 + v < d ? a.guess0[p * a.ldg + col0 + v] : 0.f;
 
     // ---- INIT (pass pc): D_k to g_0, ||x_k||^2 (gm), ||g_0||^2
     constexpr bool want_r = MODE == 1;
     __syncthreads();   // s_rows2 / s_osc of the previous problem consumed
-    rb_all_rows<KR, KV>(dist_row, &s_rows[pc & 1][w][0], lane);
+    if constexpr ((DBG & 64) == 0) rb_all_rows<KR, KV>(dist_row, &s_rows[pc & 1][w][0], lane);
     if constexpr (want_r) {
       // (a memory clobber: without it the LDS rows' reads of the pass above are kept live
       // for this one — 18 float4 beside the tile)
@@ -554,6 +572,10 @@ static const void* rb_kernel(int kr, int mode) {
       case 8: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 8>);
       case 16: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 16>);
       case 31: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 31>);
+      case 32: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 32>);
+      case 64: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 64>);
+      case 128: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 128>);
+      case 256: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 256>);
       default: break;
     }
   }
