@@ -41,6 +41,12 @@ constexpr int kRbCols = 2048;                    // columns per block
 #ifndef GMK_RB_COEF_WAVE0
 #define GMK_RB_COEF_WAVE0 0
 #endif
+// GMK_RB_PREFETCH_ROWS = n > 0: during iteration it of problem p, the rows
+// [n·it, n·it + n) of the group's NEXT problem are read into a junk LDS line (LDS-DMA, no
+// registers), so that the next tile load finds them in the Infinity Cache (A/B)
+#ifndef GMK_RB_PREFETCH_ROWS
+#define GMK_RB_PREFETCH_ROWS 0
+#endif
 #ifndef GMK_RB_OMA_ROWS
 #define GMK_RB_OMA_ROWS 2
 #endif
@@ -148,6 +154,7 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   typedef unsigned u4v __attribute__((ext_vector_type(4)));
   __shared__ f4 s_x[KL > 0 ? KL : 1][NT];
+  __shared__ f4 s_junk[GMK_RB_PREFETCH_ROWS > 0 ? 64 : 1];   // prefetch landing line
   __shared__ float s_coef[NW][KR + 2];  // each wave's own copy of the coefficients
   __shared__ float s_osc[KR];
   // row partials and the waves' movement / norm partials, by the parity of the pass they
@@ -417,6 +424,27 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
         __syncthreads();
         if (s_ok == 0) return;                       // timed out: every thread leaves
         ++pc;
+      }
+      if constexpr (GMK_RB_PREFETCH_ROWS > 0) {
+        // the next problem's rows n·it .. n·it + n - 1 into the Infinity Cache (their LDS-DMA
+        // lands in a junk line; the phases below cover the loads' latency before the next
+        // barrier drains them)
+        const int64_t pn = p + NG;
+        if (pn < a.P && it * GMK_RB_PREFETCH_ROWS < K) {
+          const uint64_t nb64 = reinterpret_cast<uint64_t>(a.X + pn * a.x_ps);
+          float* const Xn = reinterpret_cast<float*>(
+              ((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(nb64 >> 32)) << 32) |
+              (uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)nb64));
+          const int nrec = __builtin_amdgcn_readfirstlane(a.prob_bytes);
+          const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(Xn, 0, nrec, 0x00020000);
+          sfor<0, GMK_RB_PREFETCH_ROWS>([&](auto j) {
+            const int64_t kk = it * GMK_RB_PREFETCH_ROWS + j;
+            if (kk < K)
+              __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                  rn, (__attribute__((address_space(3))) void*)&s_junk[0], 16, voff,
+                  __builtin_amdgcn_readfirstlane((int)(kk * rstride * 4)), 0, 0);
+          });
+        }
       }
       // every wave: the movement / ||g||^2 sums (uniform) and, lane = client, D_k (and r_k
       // at INIT of gm), each a fixed-order sum of the G group sums
