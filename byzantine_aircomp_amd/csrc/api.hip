@@ -745,10 +745,18 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       panel_gram_rejected = true;
       algo = GM_ALGO_STREAM;
     }
+    // One problem that fits on chip (K <= 52; gm at K <= 50): the batched register-resident
+    // kernel with P = 1 reads the panels once for all iterations (the C2 kernel takes rows
+    // only).  Same eligibility as the batched call; the fused pre-noise included.
+    if ((algo == GM_ALGO_AUTO || algo == GM_ALGO_RESIDENT) && !sharded && !c->comm && !c->ar_fn) {
+      const int rc0 = run_resident_batched(c, X, 1, K, d, ldx, (d + W - 1) / W * ldx, true, W,
+                                           guess0, d, out, d, o, res, s);
+      if (rc0 != kRbNotTaken) return rc0;
+    }
     if (algo == GM_ALGO_AUTO) algo = GM_ALGO_STREAM;
     if (algo != GM_ALGO_STREAM)
-      return fail(GM_ERR_UNSUPPORTED, "panel layout: streaming or (gm2, K <= 256) Gram only "
-                  "(algo %d)", algo);
+      return fail(GM_ERR_UNSUPPORTED, "panel layout: streaming, (gm2, K <= 256) Gram or (K <= 52 "
+                  "gm2 / K <= 50 gm, unsharded) resident only (algo %d)", algo);
   }
   const int V = panels ? 4 : pick_vec(X, d, ldx);
   // AUTO: Gram-space (split bf16) for gm2 at K <= 256 on large d, kept if its

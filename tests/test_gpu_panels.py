@@ -84,17 +84,19 @@ def test_panels_store_rows_and_default_guess():
         P.store(k, X[k])
     assert torch.equal(P.to_rows(), X)
     assert torch.equal(P.row(3), X[3])
-    # (AUTO would take the register-resident kernel on the row-major input)
+    # (AUTO takes a register-resident kernel on either layout: pin the streaming pass)
     a = bz().gm2(X, {"maxiter": 20, "guess": X.mean(dim=0), "algo": "stream"})
-    b = bz().gm2(P, {"maxiter": 20, "guess": X.mean(dim=0)})
+    b = bz().gm2(P, {"maxiter": 20, "guess": X.mean(dim=0), "algo": "stream"})
     assert torch.equal(a, b)
     c = bz().gm2(P, {"maxiter": 20})          # guess = column mean of the panels
+    assert bz().aggregators.last_result.algo == "resident"
     assert rel_l2(c.cpu().numpy(), a.cpu().numpy()) <= 1e-6
 
 
 def test_panels_reject_non_streaming_algos():
-    """Panels run the streaming pass or (gm2, K <= 256) the f16 Gram; the other
-    algorithms, the f32 Gram, and Gram for AirComp gm or K > 256 raise."""
+    """Panels run the streaming pass, (gm2, K <= 256) the f16 Gram or (K <= 52) the batched
+    resident kernel; the other algorithms, the f32 Gram, Gram for AirComp gm or K > 256,
+    and "resident" at K = 64 raise."""
     X, g0 = _data(64, 512, seed=1)
     P = bz().ClientPanels.from_rows(X)
     for algo in ("twopass", "resident", "gram_f32"):
@@ -189,3 +191,30 @@ def test_gram_on_panels_overflow_falls_back_to_stream():
     assert res.algo == "stream" and res.guard == "rejected"
     assert rel_l2(got.cpu().numpy(), want.numpy()) <= 1e-5
     assert abs(res.iters - tr.iters) <= 1
+
+
+@pytest.mark.parametrize("K,d,agg", [(50, 7850, "gm2"), (1, 5, "gm2"), (20, 100_003, "gm2"),
+                                     (30, 8192, "gm"), (52, 4096, "gm2")])
+def test_single_panels_call_runs_resident(K, d, agg):
+    """One ClientPanels problem at K <= 52 (gm: K <= 50), AUTO: the batched register-resident
+    kernel with P = 1 (X read once for all iterations) instead of one streaming pass per
+    iteration; it matches the oracle (gm2) or the streaming path on the same Philox draws
+    (gm, a fixed number of iterations)."""
+    X, g0 = _data(K, d, seed=K + d)
+    P = bz().ClientPanels.from_rows(X)
+    f = getattr(bz(), agg)
+    if agg == "gm2":
+        got = f(P, {"maxiter": 1000, "tol": 1e-5, "guess": g0})
+        res = bz().aggregators.last_result
+        assert res.algo == "resident"
+        want, tr = orc.gm2(X.cpu(), {"maxiter": 1000, "tol": 1e-5, "guess": g0.cpu()})
+        assert rel_l2(got.cpu().numpy(), want.numpy()) <= 1e-5
+        assert abs(res.iters - tr.iters) <= 1
+    else:
+        opts = {"maxiter": 25, "tol": 1e-5, "guess": g0, "noise_var": 1e-2, "seed": 9}
+        got = f(P, dict(opts))
+        res = bz().aggregators.last_result
+        assert res.algo == "resident" and res.iters == 25
+        ref = f(P, dict(opts, algo="stream"))
+        assert bz().aggregators.last_result.algo == "stream"
+        assert rel_l2(got.cpu().numpy(), ref.cpu().numpy()) <= 1e-4

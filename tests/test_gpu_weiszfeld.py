@@ -462,6 +462,8 @@ def test_gram_f16_range_overflow_falls_back(spike):
     (1000, 4100, "panels", "auto"),       # fused, panels (partial last float4 group of panels)
     (300, 2051, "rows", "stream"),        # float1 rows: the standalone OMA first
     (50, 7850, "rows", "auto"),           # register-resident path: standalone OMA first
+    (50, 7850, "panels", "auto"),         # batched resident kernel, P = 1: fused in registers
+    (12, 30_001, "panels", "resident"),
     (256, 1 << 18, "rows", "auto"),       # guarded Gram: standalone OMA first
     (200, (1 << 18) + 64, "panels", "auto"),
 ])
