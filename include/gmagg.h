@@ -63,7 +63,8 @@ enum gm_noise_source {
 enum gm_layout {
     GM_LAYOUT_ROWS = 0,       /* [K][ldx] row-major (the reference's torch.stack of rows) */
     GM_LAYOUT_PANELS = 1      /* [ceil(d/W)][K][W], W = gm_panel_width(K), ldx = panel stride;
-                                 streaming, or (gm2, K <= 256, W % 64 == 0) the guarded Gram */
+                                 streaming, (gm2, K <= 256, W % 64 == 0) the guarded Gram, or
+                                 (K <= 52 gm2 / K <= 50 gm, unsharded) the resident kernel */
 };
 
 enum gm_algo {
