@@ -83,6 +83,9 @@ __device__ __forceinline__ bool rb_gather(const gu64* g, int64_t bstride, int fi
         }
       }
       if (ok) break;
+#ifndef GMK_RB_EARLY_H2
+#define GMK_RB_EARLY_H2 0
+#endif
 #ifndef GMK_RB_NOSLEEP
       __builtin_amdgcn_s_sleep(1);
 #endif
@@ -163,6 +166,7 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   __shared__ float s_rows2[NW][KR];
   __shared__ float s_fin[2][2][NW];
   __shared__ double s_part[NT];
+  __shared__ float s_rk[MODE == 1 ? NW : 1][64];   // gm: lane k's ||x_k||^2, each wave's copy
   __shared__ float s_an;
   __shared__ int s_ok;
 
@@ -388,10 +392,35 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
     __syncthreads();
     publish(want_r);
 
+    // AirComp: pass `it`'s draws depend on (problem, it, column / client) only, so each
+    // pass's are drawn right after the previous publish, while the other blocks' partials
+    // are in flight (off the gather -> phase A -> phase B chain): the column noise (M:411,
+    // one Philox block per column, one at a time: four interleaved chains beside the tile
+    // spill), lane k's channel gain |h_k|^2 (M:403) and the scalar noise of M:153-155
+    float nz[4] = {0.f, 0.f, 0.f, 0.f};
+    float h2k = 1.f, ndr = 0.f;
+    auto draw_pass = [&](int64_t i) {
+      if constexpr (MODE == 1) {
+        if (GMK_RB_EARLY_H2 && lane < K) {
+          float n4[4];
+          normal4(seed_p, kStreamChannel, (uint64_t)i, (uint64_t)lane, n4);
+          const float hr = n4[0] * 0.70710678118654752f, hi = n4[1] * 0.70710678118654752f;
+          h2k = hr * hr + hi * hi;
+        }
+        if (a.has_noise) {
+          ndr = normal1(seed_p, kStreamNoise, (uint64_t)i, (uint64_t)d);
+          sfor<0, 4>([&](auto v) {
+            nz[v] = normal1(seed_p, kStreamNoise, (uint64_t)i, (uint64_t)(col0 + v));
+            __builtin_amdgcn_sched_barrier(0);
+          });
+        }
+      }
+    };
+    draw_pass(0);
+
     int64_t it = 0;
-    double last_mv = NAN;
+    float last_mv = NAN;
     int conv = 0;
-    double r_k = 0.0;     // lane k: ||x_k||^2 (gm), from the INIT pass
     for (;; ++it) {
       // (1) gather pass pc: D (+ r at INIT of gm), movement, ||g||^2; G thread groups
       // each sum every G-th block (one round trip), then every wave adds the G group sums
@@ -457,13 +486,15 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
         if (kv) d2k += s_part[gi * ncol + k];
       }
       if (want_r && it == 0 && kv) {
-        r_k = 0.0;
+        // (kept in the wave's LDS copy, not a register: the AirComp tile is at the VGPR limit)
+        double r_k = 0.0;
         for (int gi = 0; gi < G; ++gi) r_k += s_part[gi * ncol + K + k];
+        s_rk[w][k] = (float)r_k;
       }
       // (2) tol test of the pass that produced g_it (M:180-183)
       if (it >= 1) {
         const float mv = (float)sqrt(mv2);
-        last_mv = (double)mv;
+        last_mv = mv;
         if (mv <= a.tol) { conv = 1; break; }
       }
       if (it == a.maxiter) break;
@@ -481,19 +512,20 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
           const float thr = (s * s) * 500.0f;                         // M:152
           double ck = 0.0;
           if (kv) {
-            float n4[4];
-            normal4(seed_p, kStreamChannel, (uint64_t)it, (uint64_t)k, n4);
-            const float hr = n4[0] * 0.70710678118654752f, hi = n4[1] * 0.70710678118654752f;
-            const float h2 = hr * hr + hi * hi;                       // M:403
+            float h2 = h2k;                                           // M:403 (draw_pass)
+            if constexpr (!GMK_RB_EARLY_H2) {
+              float n4[4];
+              normal4(seed_p, kStreamChannel, (uint64_t)it, (uint64_t)k, n4);
+              const float hr = n4[0] * 0.70710678118654752f, hi = n4[1] * 0.70710678118654752f;
+              h2 = hr * hr + hi * hi;
+            }
             const float dist = clamp_dist(d2k, a.eps);
-            const float pk = ((float)r_k + s * s) / (dist * dist * (float)(d + 1)) / h2;   // M:404
+            const float pk = (s_rk[w][k] + s * s) / (dist * dist * (float)(d + 1)) / h2;   // M:404
             const float pup = pk != pk ? pk : fmaxf(pk, thr);          // M:405
             ck = (double)(sqrtf((float)a.P_max / pup) / dist);         // M:407
           }
           const double Sc = xlane_wave_sum(ck);
-          const double nd = !a.has_noise ? 0.0
-                            : a.noise_sd * (double)normal1(seed_p, kStreamNoise, (uint64_t)it,
-                                                           (uint64_t)d);
+          const double nd = !a.has_noise ? 0.0 : a.noise_sd * (double)ndr;
           const double scale = (double)s / ((double)s * Sc + nd);     // M:153-155
           if (k < KR) s_coef[w][k] = kv ? (float)(ck * scale) : 0.f;
           an = a.has_noise ? (float)(scale * a.noise_sd) : 0.f;
@@ -540,17 +572,7 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
       }
       float mvp = 0.f, gnp = 0.f;
       const float gnew4[4] = {ga[0], ga[1], gb[0], gb[1]};
-      // AirComp: the column noise of pass `it` (M:411), one Philox block per column, one
-      // at a time (four interleaved Philox chains beside the tile spill)
-      float nz[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (MODE == 1) {
-        if (a.has_noise) {
-          sfor<0, 4>([&](auto v) {
-            nz[v] = normal1(seed_p, kStreamNoise, (uint64_t)it, (uint64_t)(col0 + v));
-            __builtin_amdgcn_sched_barrier(0);
-          });
-        }
-      }
+      // (AirComp: the column noise nz of pass `it` was drawn after the last publish)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         float gv = gnew4[v];
@@ -570,6 +592,7 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
       wave_fin(mvp, gnp);
       __syncthreads();
       if constexpr ((DBG & 16) == 0) publish(false);
+      if (it < a.maxiter) draw_pass(it + 1);
     }
 
     // ---- the problem's aggregate and state
