@@ -105,6 +105,8 @@ def _run(X, options: dict, aircomp: bool):
     pre_seed = int(opts.get("pre_oma_seed", 2021)) & 0xFFFFFFFFFFFFFFFF
     if pre_var is not None and opts.get("guess") is None:
         oma_batched(X, float(pre_var), seed=pre_seed)
+        if X is not X_in:
+            X_in.copy_(X)      # OMA is in place on the caller's problems (M:351-352)
         pre_var = None
     guess = opts.get("guess")
     if guess is None:

@@ -177,3 +177,54 @@ def gm2_f64(X: torch.Tensor, guess: torch.Tensor, maxiter: int = 200, tol: float
         if moved <= tol:
             break
     return g, WeiszfeldTrace(n, moved)
+
+
+@dataclass
+class CountWindow:
+    """The iteration counts an fp32 Weiszfeld may legitimately stop at on one input."""
+
+    early: int            # first t whose fp64 movement is <= tol + delta_t
+    late: int             # first t whose fp64 movement is <= tol - delta_t (maxiter if none)
+    max_norm: float       # max ||g_t|| over the run (sets the fp32 movement floor)
+
+    @property
+    def width(self) -> int:
+        return self.late - self.early
+
+
+def gm2_count_window(X: torch.Tensor, guess: Optional[torch.Tensor] = None, maxiter: int = 200,
+                     tol: float = 1e-5, floor_ulps: float = 4.0) -> CountWindow:
+    """Is "the same iteration count +-1" (north_star) well posed on this input?
+
+    The reference stops at the first t with ||g_t - g_{t+1}|| <= tol (M:180-183), on
+    fp32 iterates.  An fp32 iterate carries an error of a few ulps of its elements, so
+    the movement an fp32 implementation computes differs from the exact one by up to
+    delta_t ~ floor_ulps * 2^-24 * ||g_t|| (summation order decides the sign).  Any
+    count between ``early`` (exact movement <= tol + delta) and ``late`` (exact
+    movement <= tol - delta) is then a legitimate stopping point, for the reference as
+    for a kernel: two fp32 implementations agree to +-1 only if ``late - early <= 1``.
+    A wider window means tol sits on the fp32 movement floor and the count measures
+    rounding, not the algorithm (6 vs 8 at ||g|| ~ 8, tol 1e-6).
+    Runs the exact (fp64) iteration until the movement is below tol - delta."""
+    X64 = X.double()
+    g = (X64.mean(dim=0) if guess is None else guess.double())
+    early = late = None
+    max_norm = float(torch.linalg.vector_norm(g))
+    for t in range(1, maxiter + 1):
+        dist = torch.clamp(torch.linalg.vector_norm(X64 - g, dim=1), min=CLAMP)
+        w = 1.0 / dist
+        nxt = (w @ X64) / w.sum()
+        moved = float(torch.linalg.vector_norm(g - nxt))
+        max_norm = max(max_norm, float(torch.linalg.vector_norm(nxt)))
+        delta = floor_ulps * 2.0 ** -24 * max_norm
+        g = nxt
+        if early is None and moved <= tol + delta:
+            early = t
+        if moved <= tol - delta:
+            late = t
+            break
+        if not math.isfinite(moved) or (early is not None and tol - delta <= 0):
+            break                   # (tol below the floor: no count is certain)
+    early = maxiter if early is None else early
+    late = maxiter if late is None else late
+    return CountWindow(early, late, max_norm)

@@ -71,6 +71,35 @@ def oma_philox(X: np.ndarray, noise_var: float, seed: int, col_off: int = 0) -> 
     return X.astype(np.float64) + scale[:, None] * pick
 
 
+STREAM_FILL = 0x46494C4C
+
+
+def fill_clients(K: int, d: int, B: int, mu_h: float, sd_h: float, mu_b: float, sd_b: float,
+                 seed: int, col_off: int = 0) -> np.ndarray:
+    """The synthetic client matrix of ``gm_fill_clients_f32`` (oma.hip fill_clients):
+    element (k, global column c) = mu + sd * normal c & 3 of block (iteration k, index
+    c >> 2) on the fill stream; the last B rows take (mu_b, sd_b).  float32 of the
+    float64 Box-Muller: the device's fast sin/cos put it within ~1e-6 of this, enough
+    to decide whether a test input is well posed (tests/test_iteration_wellposed.py)."""
+    cols = col_off + np.arange(d, dtype=np.uint64)
+    X = np.empty((K, d), dtype=np.float32)
+    for k in range(K):
+        z = normal4(seed, STREAM_FILL, np.uint64(k), cols >> np.uint64(2))     # [d, 4]
+        v = np.take_along_axis(z, (cols & np.uint64(3)).astype(np.int64)[:, None], axis=1)[:, 0]
+        mu, sd = (mu_b, sd_b) if k >= K - B else (mu_h, sd_h)
+        X[k] = (mu + sd * v).astype(np.float32)
+    return X
+
+
+def fill_normal(n: int, mu: float, sd: float, seed: int, off: int = 0) -> np.ndarray:
+    """``gm_fill_normal_f32`` (oma.hip fill_normal): normal c & 3 of block
+    (iteration 0xFFFFFFFF, index c >> 2)."""
+    cols = off + np.arange(n, dtype=np.uint64)
+    z = normal4(seed, STREAM_FILL, np.uint64(0xFFFFFFFF), cols >> np.uint64(2))
+    v = np.take_along_axis(z, (cols & np.uint64(3)).astype(np.int64)[:, None], axis=1)[:, 0]
+    return (mu + sd * v).astype(np.float32)
+
+
 STREAM_CHANNEL = 0x43484E4C
 STREAM_NOISE = 0x4E4F4953
 

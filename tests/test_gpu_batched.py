@@ -19,7 +19,10 @@ def _problems(P, K, d, seed):
     return X, p[:, 0, :]
 
 
-@pytest.mark.parametrize("P,K,d", [(1, 50, 7852), (7, 50, 10_000), (12, 17, 333), (33, 64, 4096)])
+ORACLE_SHAPES = [(1, 50, 7852), (7, 50, 10_000), (12, 17, 333), (33, 64, 4096)]
+
+
+@pytest.mark.parametrize("P,K,d", ORACLE_SHAPES)
 def test_gm2_batched_matches_oracle(P, K, d):
     from byzantine_aircomp_amd.batched import gm2_batched
     X, p = _problems(P, K, d, seed=P * 100 + K)
@@ -44,16 +47,26 @@ def test_gm_batched_equals_single_calls():
         assert res[i].iters == 30
 
 
-def test_batched_mixed_convergence():
-    """Problems converge at different iterations; each stops at its own tol test."""
-    from byzantine_aircomp_amd.batched import gm2_batched
+def _mixed_problems():
     X, p = _problems(5, 30, 2048, seed=8)
-    X[2] = torch.randn(30, 2048)            # a harder problem: converges later
-    out, res = gm2_batched(X.cuda(), {"maxiter": 1000, "guess": p.cuda(), "tol": 1e-6})
+    # a harder problem (converges later), seeded: the round-3 version drew it from the
+    # global generator, so the input depended on what ran before in the process
+    X[2] = torch.randn(30, 2048, generator=torch.Generator().manual_seed(88))
+    return X, p
+
+
+def test_batched_mixed_convergence():
+    """Problems converge at different iterations; each stops at its own tol test.
+    tol 1e-5, not 1e-6: problem 2's ||g|| ~ 8 puts the fp32 movement floor
+    (~4 * 2^-24 * ||g|| = 2e-6) above 1e-6, where the count measures rounding
+    (oracle.gm2_count_window; tests/test_iteration_wellposed.py checks every +-1 input)."""
+    from byzantine_aircomp_amd.batched import gm2_batched
+    X, p = _mixed_problems()
+    out, res = gm2_batched(X.cuda(), {"maxiter": 1000, "guess": p.cuda(), "tol": 1e-5})
     iters = [r.iters for r in res]
     assert len(set(iters)) > 1
     for i in range(5):
-        want, tr = orc.gm2(X[i].clone(), {"maxiter": 1000, "tol": 1e-6, "guess": p[i].clone()})
+        want, tr = orc.gm2(X[i].clone(), {"maxiter": 1000, "tol": 1e-5, "guess": p[i].clone()})
         assert rel_l2(out[i].cpu().numpy(), want.numpy()) <= 1e-5
         assert abs(iters[i] - tr.iters) <= 1
 
@@ -89,8 +102,19 @@ def test_c5_prenoise_reading_matches_oracle():
         assert abs(res[i].iters - tr.iters) <= 1
 
 
-@pytest.mark.parametrize("K,d", [(50, 7850), (50, 4099), (200, 3000), (7, 513), (20, 4096),
-                                 (100, 2048)])
+PANEL_SHAPES = [(50, 7850), (50, 4099), (200, 3000), (7, 513), (20, 4096), (100, 2048)]
+
+
+def _panel_problems(K, d):
+    P = 5
+    g = torch.Generator().manual_seed(K * 3 + d)
+    X = 0.05 * torch.randn(P, K, d, generator=g)
+    X[:, K - K // 5:] += 0.25
+    g0 = 0.01 * torch.randn(P, d, generator=g)
+    return X, g0
+
+
+@pytest.mark.parametrize("K,d", PANEL_SHAPES)
 @pytest.mark.parametrize("agg", ["gm2", "gm"])
 def test_batched_panels_match_rows(K, d, agg):
     """ProblemPanels (every problem in the panel layout) vs the row-major batched call:
@@ -98,11 +122,9 @@ def test_batched_panels_match_rows(K, d, agg):
     128 < K <= 256),
     equal to rounding otherwise; batched OMA identical draw for draw."""
     from byzantine_aircomp_amd.batched import ProblemPanels, gm2_batched, gm_batched, oma_batched
-    P = 5
-    g = torch.Generator().manual_seed(K * 3 + d)
-    X = (0.05 * torch.randn(P, K, d, generator=g)).cuda()
-    X[:, K - K // 5:] += 0.25
-    g0 = (0.01 * torch.randn(P, d, generator=g)).cuda()
+    X, g0 = _panel_problems(K, d)
+    P = X.shape[0]
+    X, g0 = X.cuda(), g0.cuda()
     Pn = ProblemPanels.from_rows(X)
     assert torch.equal(Pn.to_rows(), X)
     oma_batched(X, 1e-2, seed=5)
@@ -152,3 +174,33 @@ def test_batched_gm_rows_staged_as_panels():
         single = bz.gm(X[i], dict(opts, guess=g0[i], seed=(11 + i * SEED_STRIDE) % 2 ** 64,
                                   algo="stream"))
         assert rel_l2(a[i].cpu().numpy(), single.cpu().numpy()) <= 1e-5
+
+
+def iteration_cases():
+    """Every input above whose iteration count is asserted +-1, built on the CPU
+    (tests/test_iteration_wellposed.py): (id, thunk -> [(X, guess, maxiter, tol), ...])."""
+    from oracle.philox import oma_philox
+    SEED_STRIDE = 0x9E3779B97F4A7C15
+    cases = []
+    for P, K, d in ORACLE_SHAPES:
+        def t(P=P, K=K, d=d):
+            X, p = _problems(P, K, d, seed=P * 100 + K)
+            return [(X[i], p[i], 1000, 1e-5) for i in range(P)]
+        cases.append((f"oracle_{P}x{K}x{d}", t))
+
+    def mixed():
+        X, p = _mixed_problems()
+        return [(X[i], p[i], 1000, 1e-5) for i in range(5)]
+    cases.append(("mixed_convergence", mixed))
+
+    def prenoise():
+        X, p = _problems(4, 50, 8192, seed=23)
+        return [(torch.from_numpy(oma_philox(X[i].numpy(), 1e-3, (7 + i * SEED_STRIDE) % 2 ** 64))
+                 .float(), p[i], 1000, 1e-5) for i in range(4)]
+    cases.append(("c5_prenoise", prenoise))
+    for K, d in PANEL_SHAPES:
+        def t(K=K, d=d):
+            X, g0 = _panel_problems(K, d)
+            return [(X[i], g0[i], 40, 1e-5) for i in range(X.shape[0])]
+        cases.append((f"panels_{K}x{d}", t))
+    return cases

@@ -138,3 +138,23 @@ def test_c5_aircomp_gm_full_batch(var):
         got = out[p].cpu().numpy()
         err32, err64, ref_err = rel_l2(got, want32), rel_l2(got, want64), rel_l2(want32, want64)
         assert err32 <= 1e-5 or err64 <= ref_err, (p, err32, err64, ref_err)
+
+
+def iteration_cases():
+    """The sampled problems of test_c5_prenoise_gm2_full_batch (device fill and fused
+    pre-noise restated by oracle/philox) for tests/test_iteration_wellposed.py."""
+    from oracle.philox import fill_clients, fill_normal, oma_philox
+    SEED_STRIDE = 0x9E3779B97F4A7C15
+    cases = []
+    for var in (1e-3, 1e-1):
+        def t(var=var):
+            P, seed = 1024, 5000
+            out = []
+            for p in _sample(P):
+                g0 = fill_normal(D, 0.0, 0.01, seed + 777, off=p * D)   # row p of [P, D]
+                X = fill_clients(K, D, BYZ[p % 3], 0.0, 0.05, 0.25, 0.5, seed + p)
+                Xn = oma_philox(X, var, (77 + p * SEED_STRIDE) % 2 ** 64).astype(np.float32)
+                out.append((torch.from_numpy(Xn), torch.from_numpy(g0), 1000, 1e-5))
+            return out
+        cases.append((f"prenoise_var{var}", t))
+    return cases

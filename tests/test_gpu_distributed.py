@@ -193,3 +193,13 @@ def test_sharded_pre_oma_world1(world1, layout):
     Bn = B.to_rows() if layout == "panels" else B
     assert torch.equal(Bn, A)
     assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-6
+
+
+def iteration_cases():
+    """(tests/test_iteration_wellposed.py) The +-1 inputs above are the device-filled C3 /
+    C4 recipes at 1000 x 200k and 256 x 2^19: too large for the CPU restatement of the
+    fill within the CPU suite.  Their ||g|| (the GM of N(0, 0.05^2) rows: ~0.0018 sqrt(d)
+    = 0.8 at K = 1000, ~0.0066 sqrt(d) = 4.8 at K = 256) puts the fp32 movement floor
+    (4 * 2^-24 ||g||) at 2e-7 / 1.1e-6, well under tol = 1e-5; the same recipe at
+    1000 x 65,536 is checked through test_gpu_fullsize.iteration_cases."""
+    return []

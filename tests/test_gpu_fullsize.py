@@ -153,3 +153,19 @@ def test_workspace_ordered_across_streams():
             b = m.gm2(Y, {"maxiter": 1000, "guess": h0, "check_every": 1})
         torch.cuda.synchronize()
         assert torch.equal(a, ref_x) and torch.equal(b, ref_y)
+
+
+def iteration_cases():
+    """The C3 tile's +-1 input (device fill restated by oracle/philox.fill_clients) for
+    tests/test_iteration_wellposed.py.  The full-size C3 / C4-shard inputs (1000 x 11M,
+    256 x 15.6M) are beyond the CPU: their +-1 compares two GPU paths, ||g|| = 5.9 / 26
+    gives a floor of 1.4e-6 / 6.2e-6 against tol 1e-5 (the C4 shard is the closest; its
+    Gram guard demands floor < tol/3 on the 2-ulp floor)."""
+    from oracle.philox import fill_clients, fill_normal
+
+    def c3_tile():
+        K, d = 1000, 65_536
+        X = torch.from_numpy(fill_clients(K, d, 200, 0.0, 0.05, 0.25, 0.5, 20211))
+        g0 = torch.from_numpy(fill_normal(d, 0.0, 0.01, 20212))
+        return [(X, g0, 1000, 1e-5)]
+    return [("c3_tile", c3_tile)]

@@ -41,8 +41,11 @@ def _to(X, layout):
 
 # K: every row tile (16 / 32 rows in VGPRs; 52 = 36 in VGPRs + 16 in LDS) and its edges;
 # d: a partial float4 group, one block, block edges, several blocks, C2's and C5's d
-@pytest.mark.parametrize("K,d", [(1, 100), (3, 5), (16, 2048), (17, 2049), (32, 4097),
-                                 (33, 7850), (50, 7851), (50, 100_000), (52, 20_000)])
+RES_SHAPES = [(1, 100), (3, 5), (16, 2048), (17, 2049), (32, 4097), (33, 7850), (50, 7851),
+              (50, 100_000), (52, 20_000)]
+
+
+@pytest.mark.parametrize("K,d", RES_SHAPES)
 @pytest.mark.parametrize("layout", ["rows", "panels"])
 def test_resident_gm2_matches_oracle(K, d, layout):
     from byzantine_aircomp_amd.batched import gm2_batched
@@ -57,14 +60,21 @@ def test_resident_gm2_matches_oracle(K, d, layout):
         assert abs(res[i].iters - tr.iters) <= 1
 
 
+def _many_problems():
+    X, p = _problems(37, 50, 60_000, seed=11)
+    # a slower problem in the middle of a group's queue (seeded: round 3 drew it from the
+    # global generator)
+    X[5] = torch.randn(50, 60_000, generator=torch.Generator().manual_seed(55))
+    return X, p
+
+
 @pytest.mark.parametrize("layout", ["rows", "panels"])
 def test_resident_many_problems_per_group(layout):
     """More problems than groups in flight: each group runs several problems back to back
     (its pass counter and granule buffers carry over); vs the streaming batched path."""
     from byzantine_aircomp_amd.batched import gm2_batched
-    P, K, d = 37, 50, 60_000
-    X, p = _problems(P, K, d, seed=11)
-    X[5] = torch.randn(K, d)          # a slower problem in the middle of a group's queue
+    X, p = _many_problems()
+    P = X.shape[0]
     # (tol 1e-5: at ||g|| ~ 17 the reference's own fp32 movement has a noise floor of
     # ~2e-6, so a tol of 1e-6 would pin rounding, not the algorithm; DESIGN.md §3.2)
     opts = {"maxiter": 1000, "guess": p.cuda(), "tol": 1e-5}
@@ -81,8 +91,11 @@ def test_resident_many_problems_per_group(layout):
         assert abs(res_r[i].iters - tr.iters) <= 1
 
 
+PRENOISE_SHAPES = [(50, 30_001), (12, 4096)]
+
+
 @pytest.mark.parametrize("layout", ["rows", "panels"])
-@pytest.mark.parametrize("K,d", [(50, 30_001), (12, 4096)])
+@pytest.mark.parametrize("K,d", PRENOISE_SHAPES)
 def test_resident_fused_prenoise_is_oma(layout, K, d):
     """gm2 --var v: the pre-noise applied in registers and written back equals the
     standalone batched OMA bit for bit; the aggregates match OMA then gm2 (streaming)."""
@@ -185,3 +198,33 @@ def test_resident_rows_and_panels_identical(agg, K, d):
     b, rb = f(_to(X, "panels"), dict(opts))
     assert torch.equal(a, b)
     assert [r.iters for r in ra] == [r.iters for r in rb]
+
+
+def iteration_cases():
+    """The +-1 inputs above, on the CPU (tests/test_iteration_wellposed.py)."""
+    from oracle.philox import oma_philox
+    SEED_STRIDE = 0x9E3779B97F4A7C15
+    cases = []
+    for K, d in RES_SHAPES:
+        def t(K=K, d=d):
+            X, p = _problems(3, K, d, seed=K * 1000 + d)
+            return [(X[i], p[i], 1000, 1e-5) for i in range(3)]
+        cases.append((f"oracle_{K}x{d}", t))
+
+    def many():
+        X, p = _many_problems()
+        return [(X[i], p[i], 1000, 1e-5) for i in range(X.shape[0])]
+    cases.append(("many_problems", many))
+    for K, d in PRENOISE_SHAPES:
+        def t(K=K, d=d):
+            X, p = _problems(9, K, d, seed=3 + K)
+            return [(torch.from_numpy(oma_philox(X[i].numpy(), 1e-2,
+                                                 (77 + i * SEED_STRIDE) % 2 ** 64)).float(),
+                     p[i], 1000, 1e-5) for i in range(9)]
+        cases.append((f"prenoise_{K}x{d}", t))
+
+    def strided():
+        X, p = _problems(4, 40, 10_000, seed=21)
+        return [(X[i], p[i], 1000, 1e-5) for i in range(4)]
+    cases.append(("strided", strided))
+    return cases

@@ -18,11 +18,16 @@ from conftest import rel_l2
 pytestmark = pytest.mark.gpu
 
 
-def _problem(K, d, B, seed):
+def _problem_cpu(K, d, B, seed):
     g = torch.Generator().manual_seed(seed)
     p = 0.07 * torch.randn(d, generator=g)
     X = p + 5e-4 * torch.randn(K, d, generator=g)
     X[K - B:] = p + 5e-3 * torch.randn(B, d, generator=g) + 2e-3
+    return X, p
+
+
+def _problem(K, d, B, seed):
+    X, p = _problem_cpu(K, d, B, seed)
     return X.cuda(), p.cuda()
 
 
@@ -152,18 +157,23 @@ def test_sharded_lagged_poll_equals_unsharded(P):
     assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-6
 
 
+def _gram_data():
+    K, d = 64, 2 * (1 << 18) + 4096
+    g = torch.Generator().manual_seed(21)         # C4 recipe: the guard keeps the Gram result
+    X = 0.05 * torch.randn(K, d, generator=g)
+    X[K - 12:] = 0.25 + 0.5 * torch.randn(12, d, generator=g)
+    return X, 0.01 * torch.randn(d, generator=g)
+
+
 @pytest.mark.parametrize("algo", [0, 3])          # AUTO (guarded Gram) and explicit split Gram
 def test_sharded_gram_equals_unsharded(algo):
     """d-sharded Gram: one all-reduce of G (and of the closing pass's sums for the
     guard); every rank takes the same guard decision."""
     import byzantine_aircomp_amd as bz
     from byzantine_aircomp_amd import _lib
-    K, P = 64, 2
-    d = 2 * (1 << 18) + 4096
-    g = torch.Generator().manual_seed(21)         # C4 recipe: the guard keeps the Gram result
-    X = 0.05 * torch.randn(K, d, generator=g)
-    X[K - 12:] = 0.25 + 0.5 * torch.randn(12, d, generator=g)
-    X, p = X.cuda(), (0.01 * torch.randn(d, generator=g)).cuda()
+    P = 2
+    X, p = _gram_data()
+    X, p = X.cuda(), p.cuda()
     opts = {"maxiter": 1000, "tol": 1e-5}
     want = bz.gm2(X, dict(opts, guess=p, algo="stream"))
     n = bz.aggregators.last_result.iters
@@ -225,7 +235,7 @@ def test_oma_philox_shard_invariant(cuts):
         ctx.close()
 
 
-@pytest.mark.parametrize("K,d,P,algo,want_algo", [
+RAGGED = [
     # 1000 x 50002 over 3: shards 16896 / 16896 / 16210 columns (last ragged, d % 4 = 2);
     # K * d_local straddles the 2^24 poll threshold, K * d_total does not
     (1000, 50_002, 3, 0, {1}),
@@ -234,17 +244,25 @@ def test_oma_philox_shard_invariant(cuts):
     (200, (1 << 18) + 1024, 3, 0, {3}),
     # d_total % 4 == 2: no Gram anywhere, although the first shards are float4-aligned
     (200, (1 << 18) + 1026, 3, 0, {1}),
-])
+]
+
+
+def _ragged_data(K, d):
+    g = torch.Generator().manual_seed(d % 1000)    # the C3/C4 recipe
+    B = K // 5
+    X = 0.05 * torch.randn(K, d, generator=g)
+    X[K - B:] = 0.25 + 0.5 * torch.randn(B, d, generator=g)
+    return X, 0.01 * torch.randn(d, generator=g)
+
+
+@pytest.mark.parametrize("K,d,P,algo,want_algo", RAGGED)
 def test_sharded_ragged_last_shard_same_decisions(K, d, P, algo, want_algo):
     """Every rank must issue the same sequence of all-reduces: the
     Gram/streaming choice and the poll interval come from K, d_total and the
     options, never from the local slice."""
     import byzantine_aircomp_amd as bz
-    g = torch.Generator().manual_seed(d % 1000)    # the C3/C4 recipe (BASELINE.md §3)
-    B = K // 5
-    X = 0.05 * torch.randn(K, d, generator=g)
-    X[K - B:] = 0.25 + 0.5 * torch.randn(B, d, generator=g)
-    X, p = X.cuda(), (0.01 * torch.randn(d, generator=g)).cuda()
+    X, p = _ragged_data(K, d)
+    X, p = X.cuda(), p.cuda()
     opts = {"maxiter": 1000, "tol": 1e-5}
     want = bz.gm2(X, dict(opts, guess=p, algo="stream"))
     n = bz.aggregators.last_result.iters
@@ -252,3 +270,15 @@ def test_sharded_ragged_last_shard_same_decisions(K, d, P, algo, want_algo):
     assert len(iters) == 1 and abs(iters.pop() - n) <= 1
     assert _sharded.algos == want_algo
     assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-5
+
+
+def iteration_cases():
+    """The +-1 inputs above, on the CPU (tests/test_iteration_wellposed.py)."""
+    cases = []
+    for seed in (2, 3, 4, 12, 13):          # test_sharded_gm2_equals_unsharded, lagged poll
+        cases.append((f"sgd_seed{seed}",
+                      lambda seed=seed: [(*_problem_cpu(200, 50_000, 40, seed), 1000, 1e-5)]))
+    cases.append(("gram", lambda: [(*_gram_data(), 1000, 1e-5)]))
+    for K, d in sorted({(K, d) for K, d, *_ in RAGGED}):
+        cases.append((f"ragged_{K}x{d}", lambda K=K, d=d: [(*_ragged_data(K, d), 1000, 1e-5)]))
+    return cases

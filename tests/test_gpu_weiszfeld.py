@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden_case, golden_names, rel_l2
+from conftest import assert_iter_count, fixture_window, golden_case, golden_names, rel_l2
 from oracle import aggregators as orc
 
 pytestmark = pytest.mark.gpu
@@ -46,7 +46,7 @@ def test_gm2_matches_reference(name, algo):
         return
     assert out.device.type == "cuda" and out.dtype == torch.float32
     assert rel_l2(out.cpu().numpy(), arr["out"]) <= TOL
-    assert abs(res.iters - meta["iters"]) <= ITER_SLACK
+    assert_iter_count(res.iters, meta["iters"], fixture_window(name))
     assert torch.equal(X.cpu(), torch.from_numpy(arr["X"]))   # wList not mutated
 
 
@@ -63,7 +63,8 @@ def test_gm2_clamp_and_duplicates():
     meta, arr = golden_case("gm2_clamp_duplicates")
     out = bz().gm2(torch.from_numpy(arr["X"]).cuda(), _opts(meta, arr))
     assert rel_l2(out.cpu().numpy(), arr["out"]) <= TOL
-    assert abs(bz().aggregators.last_result.iters - meta["iters"]) <= ITER_SLACK
+    assert_iter_count(bz().aggregators.last_result.iters, meta["iters"],
+                      fixture_window("gm2_clamp_duplicates"))
 
 
 @pytest.mark.parametrize("name", golden_names("gm"))
@@ -216,15 +217,24 @@ def test_gm_rows_staged_as_panels(K, d, pad, exact):
         assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 1e-5
 
 
-@pytest.mark.parametrize("K", [1, 2, 16, 17, 33, 64, 65, 129, 257, 513, 1000, 1025, 2049])
-@pytest.mark.parametrize("d", [1, 6, 4099])
-def test_gm2_shapes_vs_oracle(K, d):
-    g = torch.Generator().manual_seed(K * 7919 + d)
+SHAPE_K = [1, 2, 16, 17, 33, 64, 65, 129, 257, 513, 1000, 1025, 2049]
+SHAPE_D = [1, 6, 4099]
+
+
+def _sgd_like(K, d, seed):
+    g = torch.Generator().manual_seed(seed)
     p = 0.07 * torch.randn(d, generator=g)
     X = p + 5e-4 * torch.randn(K, d, generator=g)
     B = K // 5
     if B:
         X[K - B:] += 5e-3 * torch.randn(B, d, generator=g) + 2e-3
+    return X, p
+
+
+@pytest.mark.parametrize("K", SHAPE_K)
+@pytest.mark.parametrize("d", SHAPE_D)
+def test_gm2_shapes_vs_oracle(K, d):
+    X, p = _sgd_like(K, d, K * 7919 + d)
     opts = {"maxiter": 1000, "tol": 1e-5, "guess": p.clone()}
     want, tr = orc.gm2(X.clone(), dict(opts))
     got = bz().gm2(X.cuda(), dict(opts, guess=p.cuda()))
@@ -243,7 +253,7 @@ def test_gm2_strided_rows():
 
 
 def test_gm2_nan_runs_to_maxiter():
-    X = torch.randn(8, 100)
+    X = torch.randn(8, 100, generator=torch.Generator().manual_seed(8))
     X[3, 7] = float("nan")
     out = bz().gm2(X.cuda(), {"maxiter": 13})
     assert bz().aggregators.last_result.iters == 13
@@ -254,7 +264,8 @@ def test_gm2_default_options_mean_guess():
     meta, arr = golden_case("gm2_defaults")
     out = bz().gm2(torch.from_numpy(arr["X"]).cuda())
     assert rel_l2(out.cpu().numpy(), arr["out"]) <= TOL
-    assert abs(bz().aggregators.last_result.iters - meta["iters"]) <= ITER_SLACK
+    assert_iter_count(bz().aggregators.last_result.iters, meta["iters"],
+                      fixture_window("gm2_defaults"))
 
 
 def test_gm2_translation_and_permutation_invariance():
@@ -316,19 +327,18 @@ def test_gram_matches_reference(name, algo):
     res = bz().aggregators.last_result
     assert res.algo == algo
     assert rel_l2(out.cpu().numpy(), arr["out"]) <= TOL
-    assert abs(res.iters - meta["iters"]) <= ITER_SLACK
+    assert_iter_count(res.iters, meta["iters"], fixture_window(name))
+
+
+GRAM_K = [1, 8, 32, 33, 64, 100, 128, 200, 256]
+GRAM_D = [4, 4096, 100_000]
 
 
 @pytest.mark.parametrize("algo", ["gram", "gram_f32"])
-@pytest.mark.parametrize("K", [1, 8, 32, 33, 64, 100, 128, 200, 256])
-@pytest.mark.parametrize("d", [4, 4096, 100_000])
+@pytest.mark.parametrize("K", GRAM_K)
+@pytest.mark.parametrize("d", GRAM_D)
 def test_gram_shapes_vs_oracle(K, d, algo):
-    g = torch.Generator().manual_seed(K * 31 + d)
-    p = 0.07 * torch.randn(d, generator=g)
-    X = p + 5e-4 * torch.randn(K, d, generator=g)
-    B = K // 5
-    if B:
-        X[K - B:] += 5e-3 * torch.randn(B, d, generator=g) + 2e-3
+    X, p = _sgd_like(K, d, K * 31 + d)
     opts = {"maxiter": 1000, "tol": 1e-5, "guess": p.clone()}
     want, tr = orc.gm2(X.clone(), dict(opts))
     got = bz().gm2(X.cuda(), dict(opts, guess=p.cuda(), algo=algo))
@@ -385,25 +395,30 @@ def test_gram_split_vs_f32_and_auto_choice():
     assert rel_l2(c.cpu().numpy(), b.cpu().numpy()) <= 1e-6   # closing-pass tiles differ
 
 
-@pytest.mark.parametrize("case", ["far_offset", "tight_cluster", "g_error"])
+GUARD_CASES = ["far_offset", "tight_cluster", "g_error"]
+
+
+def _guard_data(case):
+    g = torch.Generator().manual_seed(11)
+    K, d = 64, 1 << 18
+    if case == "far_offset":
+        X = 3.0 + 0.05 * torch.randn(K, d, generator=g)
+    elif case == "tight_cluster":
+        X = 1.0 + 1e-3 * torch.randn(K, d, generator=g)
+        X[50:] += 0.05
+    else:            # ||g|| small enough for the floor test; D_k ~ 1e-7 G_kk
+        X = 0.05 + 1e-5 * torch.randn(K, d, generator=g)
+    return X, torch.zeros(d)
+
+
+@pytest.mark.parametrize("case", GUARD_CASES)
 def test_gram_guard_falls_back_to_streaming(case):
     """Data where the Gram may not reproduce the reference: the reference's fp32
     movement floor ~2^-24 ||g|| exceeds tol/3 (AUTO must run the streaming path),
     or D_k ~ 1e-7 G_kk (the a-posteriori check decides; either way the result
     must match the oracle)."""
     m = bz()
-    g = torch.Generator().manual_seed(11)
-    K, d = 64, 1 << 18
-    if case == "far_offset":
-        X = 3.0 + 0.05 * torch.randn(K, d, generator=g)
-        p = torch.zeros(d)
-    elif case == "tight_cluster":
-        X = 1.0 + 1e-3 * torch.randn(K, d, generator=g)
-        X[50:] += 0.05
-        p = torch.zeros(d)
-    else:            # ||g|| small enough for the floor test; D_k ~ 1e-7 G_kk
-        X = 0.05 + 1e-5 * torch.randn(K, d, generator=g)
-        p = torch.zeros(d)
+    X, p = _guard_data(case)
     opts = {"maxiter": 30, "tol": 1e-5, "guess": p}
     want, tr = orc.gm2(X.clone(), dict(opts))
     got = m.gm2(X.cuda(), dict(opts, guess=p.cuda()))
@@ -412,8 +427,9 @@ def test_gram_guard_falls_back_to_streaming(case):
         assert res.algo == "stream"
     # whichever path AUTO kept, it reproduces the reference
     assert rel_l2(got.cpu().numpy(), want.numpy()) <= TOL
-    if res.converged and tr.iters < 30:
-        assert abs(res.iters - tr.iters) <= ITER_SLACK
+    # (far_offset / tight_cluster put tol on the fp32 movement floor by design: the
+    # count is checked against the window of legitimate stopping points)
+    assert_iter_count(res.iters, tr.iters, orc.gm2_count_window(X, p, 30, 1e-5))
 
 
 def test_gram_f16_split_matches_bf16_split(monkeypatch):
@@ -431,6 +447,15 @@ def test_gram_f16_split_matches_bf16_split(monkeypatch):
     assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 1e-6
 
 
+def _spike_data(spike):
+    g = torch.Generator().manual_seed(5)
+    K, d = 64, 1 << 18
+    X = 0.05 * torch.randn(K, d, generator=g)
+    X[K - 12:] += 0.25
+    X[5, 200_000] = spike                     # well past the first stages of its block
+    return X, torch.zeros(d)
+
+
 @pytest.mark.parametrize("spike", [1e6, float("inf")])
 def test_gram_f16_range_overflow_falls_back(spike):
     """An element far beyond the f16 headroom of its row's scale (set from the
@@ -438,12 +463,7 @@ def test_gram_f16_range_overflow_falls_back(spike):
     split (or, for a non-finite input, ends on the streaming path) and still
     matches the reference."""
     m = bz()
-    g = torch.Generator().manual_seed(5)
-    K, d = 64, 1 << 18
-    X = 0.05 * torch.randn(K, d, generator=g)
-    X[K - 12:] += 0.25
-    X[5, 200_000] = spike                     # well past the first stages of its block
-    p = torch.zeros(d)
+    X, p = _spike_data(spike)
     opts = {"maxiter": 1000, "tol": 1e-5, "guess": p}
     want, tr = orc.gm2(X.clone(), dict(opts))
     got = m.gm2(X.cuda(), dict(opts, guess=p.cuda(), algo="gram"))
@@ -576,3 +596,44 @@ def test_pre_oma_host_draws_keep_reference_sequence():
     assert after_ref == after_gpu              # the same number of CPU-generator draws
     assert torch.equal(Xg.cpu(), Xr)
     assert rel_l2(got.cpu().numpy(), want.numpy()) <= TOL
+
+
+def iteration_cases():
+    """The +-1 inputs above, on the CPU (tests/test_iteration_wellposed.py).  Not here:
+    the Gram-vs-streaming equalities at K = 256 x d = 1M / 4M on the device-filled C4
+    recipe (test_gram_matches_stream_at_c4_scale, test_gram_split_vs_f32_and_auto_choice,
+    test_gram_f16_split_matches_bf16_split): the CPU restatement of the fill is too slow
+    for the CPU suite at that size; their ||g|| (6.6 / 13) puts delta at 1.6e-6 / 3.1e-6."""
+    from conftest import golden_case, golden_names
+    cases = []
+    for name in golden_names("gm2"):
+        def t(name=name):
+            meta, arr = golden_case(name)
+            o = meta["options"]
+            guess = torch.from_numpy(arr["guess"].copy()) if meta.get("guess_supplied") else None
+            return [(torch.from_numpy(arr["X"].copy()), guess, o.get("maxiter", 200),
+                     o.get("tol", 1e-5), "windowed")]      # (assert_iter_count + window)
+        cases.append((f"golden_{name}", t))
+    for K in SHAPE_K:
+        def t(K=K):
+            out = []
+            for d in SHAPE_D:
+                X, p = _sgd_like(K, d, K * 7919 + d)
+                out.append((X, p, 1000, 1e-5))
+            return out
+        cases.append((f"shapes_K{K}", t))
+    for K in GRAM_K:
+        def t(K=K):
+            out = []
+            for d in GRAM_D:
+                X, p = _sgd_like(K, d, K * 31 + d)
+                out.append((X, p, 1000, 1e-5))
+            return out
+        cases.append((f"gram_K{K}", t))
+    for case in GUARD_CASES:
+        def t(case=case):
+            X, p = _guard_data(case)
+            return [(X, p, 30, 1e-5, "windowed")]
+        cases.append((f"guard_{case}", t))
+    cases.append(("spike", lambda: [(*_spike_data(1e6), 1000, 1e-5)]))
+    return cases
