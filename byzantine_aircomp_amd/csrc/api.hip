@@ -73,9 +73,29 @@ struct gm_ctx {
   bool ws_pending = false;
   float* stage = nullptr;   // panel copy of a row-major client matrix (gm_weiszfeld_f32)
   size_t stage_bytes = 0;
+  // A register-resident grid that failed its co-residency check-in (device_util.h
+  // grid_checkin: a shared GPU, CUs held by another stream) makes the next calls stream
+  // straight away instead of paying the check-in's 100 ms again; retried after this many.
+  int res_skip = 0;
 };
 
 namespace {
+
+constexpr int kResSkipAfterCheckinFail = 64;
+
+// Resident paths are tried unless a recent call's grid failed its check-in.
+bool resident_allowed(gm_ctx* c) {
+  if (c->res_skip <= 0) return true;
+  --c->res_skip;
+  return false;
+}
+
+// GMAGG_RES_CHECKIN_FAIL=1: the check-in waits for one slot nobody writes, so it fails
+// (tests of the fallback; read per call).
+unsigned checkin_need(unsigned blocks) {
+  const char* e = getenv("GMAGG_RES_CHECKIN_FAIL");
+  return blocks + ((e && atoi(e) != 0) ? 1u : 0u);
+}
 
 // Stream-orders the context's workspace between calls (see gm_ctx::ws_ev): the
 // constructor makes `s` wait for the previous call's tail when that call ran on
@@ -311,6 +331,8 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   a.P_max = o->P_max; a.noise_sd = std::sqrt(std::max(0.0, o->noise_var) / 2.0);
   a.seed = o->seed;
   a.gran = reinterpret_cast<unsigned long long*>(w.slab);
+  a.checkin = a.gran + (size_t)2 * nb * S;      // (resident_gran_words: + nb + 1 slots)
+  a.need = checkin_need((unsigned)nb);
   a.bar = bar; a.st = w.st;
   hipEvent_t e0, e1;
   rc = record_pass_begin(c, s, &e0, &e1);
@@ -325,6 +347,7 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   HIPCHK(hipStreamSynchronize(s));
   if (hbar[2]) {   // the grid was not co-resident long enough: caller reruns on streaming
     *timed_out = true;
+    if (!hbar[3]) c->res_skip = kResSkipAfterCheckinFail;   // failed at the check-in
     if (c->timing && !c->ev_used.empty()) {
       c->ev_free.push_back(c->ev_used.back().first);
       c->ev_free.push_back(c->ev_used.back().second);
@@ -357,6 +380,7 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
   }();
   if (!on || c->d_total > 0) return kRbNotTaken;
   if (o->mode == GM_MODE_AIRCOMP && o->noise_source != GM_NOISE_PHILOX) return kRbNotTaken;
+  if (!resident_allowed(c)) return kRbNotTaken;
   // float4 tile rows: 16-byte aligned problems, rows and panels
   if ((reinterpret_cast<uintptr_t>(X) & 15) || ldp % 4 || ldx % 4 || (panels && Wp % 4))
     return kRbNotTaken;
@@ -369,6 +393,8 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
   auto take = [&](size_t bytes) { size_t r0 = off; off = align_up(off + bytes, 256); return r0; };
   const size_t o_st = take(sizeof(KState) * P), o_flag = take(16);
   const size_t o_gran = take(sizeof(unsigned long long) * rb_gran_words(K, plan));
+  const unsigned nblocks = (unsigned)(plan.ng * plan.nb);
+  const size_t o_ci = take(sizeof(unsigned long long) * (nblocks + 1));
   if (off > c->ws_bytes) {
     if (c->ws) HIPCHK(hipFree(c->ws));
     c->ws = nullptr;
@@ -401,6 +427,8 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
   a.oma_seed = o->pre_oma_seed;
   a.gran = reinterpret_cast<unsigned long long*>(b + o_gran);
   a.flag = flag;
+  a.checkin = reinterpret_cast<unsigned long long*>(b + o_ci);
+  a.need = checkin_need(nblocks);
   a.st = st;
   hipEvent_t e0, e1;
   rc = record_pass_begin(c, s, &e0, &e1);
@@ -419,11 +447,18 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
       c->ev_free.push_back(c->ev_used.back().second);
       c->ev_used.pop_back();
     }
-    // the blocks were not co-resident long enough; with the fused pre-noise some problems
-    // may already carry their noise, so the call cannot simply be streamed again
+    // The grid was not co-resident.  Failed at the check-in (hflag[2] == 0): no block
+    // read or wrote X, the caller streams (the pre-noise fused into its INIT pass) and
+    // the next calls skip the resident kernels for a while.  Timed out after the
+    // check-in (a block descheduled for 2 s mid-call): with the fused pre-noise some
+    // problems may already carry their noise, so that call cannot be streamed again.
+    if (!hflag[2]) {
+      c->res_skip = kResSkipAfterCheckinFail;
+      return kRbNotTaken;
+    }
     if (o->pre_oma)
-      return fail(GM_ERR_HIP, "batched resident kernel timed out after the fused pre-noise "
-                  "began (another process sharing the GPU?); X is partly noised");
+      return fail(GM_ERR_HIP, "batched resident kernel timed out after its check-in, with "
+                  "the fused pre-noise begun (a block descheduled for 2 s?); X is partly noised");
     return kRbNotTaken;
   }
   if (results)
@@ -794,7 +829,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
     const int J = cfg.LPR * cfg.V;
     const int64_t nch = (d + J - 1) / J;
     int cpb = 0, nbr = 0;
-    if (resident_plan(cfg, nch, c->num_cu, &cpb, &nbr)) {
+    if (resident_allowed(c) && resident_plan(cfg, nch, c->num_cu, &cpb, &nbr)) {
       bool timed_out = false;
       int rco = apply_oma();
       if (rco) return rco;

@@ -236,4 +236,60 @@ __device__ __forceinline__ float xlane_wave_sum_f32(float v) {
   return v;
 }
 
+// Co-residency check-in of a plain-launched persistent grid (resident.hip,
+// resident_batched.hip), before a block reads or writes anything of the problem: block
+// b stores the tag into ci[b]; every block then waits, bounded by `ticks` of the 100 MHz
+// real-time clock, until slots [0, need) all carry it (need = the grid's block count;
+// GMAGG_RES_CHECKIN_FAIL makes it one more, a slot nobody writes, to test the fallback).
+// A grid that is not co-resident (a shared GPU, CUs held by another stream's kernel)
+// fails here within `ticks`, with X untouched, instead of in an iteration's 2 s poll:
+// the first block to give up raises *tmo (the kernel's timeout word), and every block —
+// including one that only starts after the others left and finds every slot written —
+// then returns.  A block that passes raises *passed before touching X, so the host can
+// tell the two cases apart.  `s_ok`: the block's shared pass / fail word.
+constexpr unsigned kCheckinTag = 0xC0DEC0DEu;
+constexpr uint64_t kCheckinTicks = 10000000ull;   // 100 ms
+
+__device__ __forceinline__ bool grid_checkin(unsigned long long* ci, unsigned need,
+                                             unsigned* tmo_word, unsigned* passed,
+                                             uint64_t ticks, int* s_ok) {
+  typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+  typedef __attribute__((address_space(1))) unsigned gu32_t;
+  gu64_t* c = (gu64_t*)ci;
+  gu32_t* tmo = (gu32_t*)tmo_word;
+  const unsigned tid = threadIdx.x;
+  if (tid == 0) {
+    *s_ok = 1;
+    __hip_atomic_store(c + blockIdx.x, (unsigned long long)kCheckinTag << 32, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  bool ok = true;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned b = tid; ok && b < need; b += blockDim.x) {
+    for (unsigned spins = 0;; ++spins) {
+      if ((unsigned)(__hip_atomic_load(c + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) ==
+          kCheckinTag)
+        break;
+      __builtin_amdgcn_s_sleep(2);
+      if (((spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > ticks) ||
+          __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = false;
+        break;
+      }
+    }
+  }
+  if (!ok) *s_ok = 0;
+  __syncthreads();
+  if (tid == 0 && *s_ok && __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    *s_ok = 0;                       // every slot written, but the grid already gave up
+  __syncthreads();
+  const bool pass = *s_ok != 0;
+  if (tid == 0 && pass)
+    __hip_atomic_store((gu32_t*)passed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_s_waitcnt(0);     // the flag stores complete before the block leaves
+  return pass;
+}
+
 }  // namespace gmk

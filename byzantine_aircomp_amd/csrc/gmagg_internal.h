@@ -116,7 +116,9 @@ struct ResArgs {
   double P_max, noise_sd;
   uint64_t seed;
   unsigned long long* gran;  // [2][gridDim.x][2K + 2] {tag, fp32} granules (zeroed per call)
-  unsigned* bar;         // [2] timeout flag (zeroed per call)
+  unsigned* bar;         // [2] timeout flag, [3] check-in passed (zeroed per call)
+  unsigned long long* checkin;   // [gridDim.x + 1] co-residency slots (zeroed per call)
+  unsigned need;         // slots the check-in waits for (gridDim.x; + 1 forces a failure)
   KState* st;
 };
 // Plan a resident launch over nch chunks: chunks per block and blocks (false: the
@@ -147,7 +149,9 @@ struct ResBArgs {
   float oma_sd;
   uint64_t oma_seed;
   unsigned long long* gran;  // [NG][2][NB][2K + 2] {tag, fp32} granules (zeroed per call)
-  unsigned* flag;         // [0] timeout flag (zeroed per call)
+  unsigned* flag;         // [0] timeout flag, [2] check-in passed (zeroed per call)
+  unsigned long long* checkin;   // [gridDim.x + 1] co-residency slots (zeroed per call)
+  unsigned need;          // slots the check-in waits for (gridDim.x; + 1 forces a failure)
   KState* st;             // [P]
 };
 struct RbPlan {

@@ -175,7 +175,8 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   const bool fin = tid < JB && gj < d;
   gu64* gran = (gu64*)a.gran;                      // [2][nb][2 NV]
   gu32* tmo = (gu32*)a.bar + 2;
-  if (tid == 0) s_ok = 1;
+  // every block of the grid co-resident before anything is read (device_util.h)
+  if (!grid_checkin(a.checkin, a.need, a.bar + 2, a.bar + 3, kCheckinTicks, &s_ok)) return;
 
   // ---- the block's tiles: loaded once, resident for the whole call
   float x[CPB][R][V];
@@ -604,7 +605,8 @@ bool resident_plan(const PassCfg& cfg, int64_t nch, int num_cu, int* cpb_out, in
 
 size_t resident_gran_words(int64_t K, const PassCfg& cfg, int nb) {
   (void)cfg;
-  return (size_t)2 * nb * (size_t)(2 * K + 2);
+  // [2][nb][2K + 2] granules, then nb + 1 co-residency check-in slots
+  return (size_t)2 * nb * (size_t)(2 * K + 2) + (size_t)nb + 1;
 }
 
 bool res_coop_launch() {

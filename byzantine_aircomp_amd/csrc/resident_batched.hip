@@ -158,7 +158,10 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   typedef unsigned u4v __attribute__((ext_vector_type(4)));
   __shared__ f4 s_x[KL > 0 ? KL : 1][NT];
   __shared__ f4 s_junk[GMK_RB_PREFETCH_ROWS > 0 ? 64 : 1];   // prefetch landing line
-  __shared__ float s_coef[NW][KR + 2];  // each wave's own copy of the coefficients
+  // each wave's own copy of the coefficients, rows padded to 16 bytes (phase A reads them
+  // as float4)
+  constexpr int KC = (KR + 2 + 3) / 4 * 4;
+  __shared__ __attribute__((aligned(16))) float s_coef[NW][KC];
   __shared__ float s_osc[KR];
   // row partials and the waves' movement / norm partials, by the parity of the pass they
   // belong to: a publish reads buffer p & 1 while the next pass's phase B fills the other
@@ -188,8 +191,10 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   // element (k, col0) of a problem: rows [k][ldx], panels [(j/W)][K][W]
   const int64_t e0 = a.pstride ? (col0 >> a.wshift) * a.pstride + (col0 & (W - 1)) : col0;
   const uint32_t voff = any ? (uint32_t)(e0 * 4) : 0x80000000u;
-  if (tid == 0) s_ok = 1;
-  if (tid < NW * (KR + 2)) (&s_coef[0][0])[tid] = 0.f;
+  if (tid < NW * KC) (&s_coef[0][0])[tid] = 0.f;
+  // every block of the grid co-resident before any problem's X is read or (pre-noise)
+  // written: a grid that is not fails here with X untouched (device_util.h)
+  if (!grid_checkin(a.checkin, a.need, a.flag, a.flag + 2, kCheckinTicks, &s_ok)) return;
 
   f4 x[KV > 0 ? KV : 1];   // the tile's register rows: row k of the thread's 4 columns
   float g[4];              // the iterate at those columns

@@ -71,10 +71,21 @@ def torch_allreduce_adapter(group=None, device: torch.device | None = None):
 
 def _aligned(shards, d_total: int) -> bool:
     """Every rank's shard lies in [0, d_total), 256-aligned at lo and 4-aligned at hi
-    (so d_total % 4 == 0 gives every rank the float4 rows the Gram path needs).  Tiling
-    is not required: a one-GPU rehearsal runs rank r's shard of a larger job alone."""
-    return all(0 <= lo <= hi <= d_total and lo % ALIGN == 0 and (hi % 4 == 0 or hi == d_total)
-               for lo, hi in shards)
+    (so d_total % 4 == 0 gives every rank the float4 rows the Gram path needs).  With
+    more than one rank the shards must also tile [0, d_total) — contiguous, no overlap,
+    no gap — or the all-reduced distances sum over the wrong set of columns; a single
+    rank may hold any shard (a one-GPU rehearsal of rank r of a larger job)."""
+    if not all(0 <= lo <= hi <= d_total and lo % ALIGN == 0 and (hi % 4 == 0 or hi == d_total)
+               for lo, hi in shards):
+        return False
+    if len(shards) == 1:
+        return True
+    end = 0
+    for lo, hi in sorted(shards):
+        if lo != end:
+            return False
+        end = hi
+    return end == d_total
 
 
 class ShardedGM:
@@ -103,7 +114,7 @@ class ShardedGM:
             if not _aligned(shards, d_total):
                 raise ValueError(f"shards {shards} of d_total={d_total}: each must be [lo, hi) "
                                  f"within [0, d_total) with lo % {ALIGN} == 0 and hi % 4 == 0 "
-                                 "(or hi == d_total)")
+                                 "(or hi == d_total), tiling [0, d_total) at world size > 1")
         self.ctx = Context(self.device.index)
         self.ctx.set_shard(d_total, self.lo)
         if transport == "rccl":

@@ -229,6 +229,14 @@ class _ClientChain:
             return f"unsupported shape (F={F}, C={C}, batch={batch})"
         if lin.weight.dtype != torch.float32:
             return "fp32 parameters only"
+        x, y = ds.tensors
+        # the kernel reads F features per sample row and trains on labels in [0, C): the
+        # torch loop raises on either mismatch, so the kernel path must not run silently
+        if x.dim() < 1 or len(x) == 0 or x[0].numel() != F:
+            return f"samples of {x[0].numel() if len(x) else 0} features, the model takes {F}"
+        if y.dim() != 1 or len(y) != len(x) or y.dtype.is_floating_point \
+                or int(y.min()) < 0 or int(y.max()) >= C:
+            return f"labels must be integers in [0, {C}), one per sample"
         return None
 
     def __init__(self, model, ds, cuts, batch, num_classes, device):

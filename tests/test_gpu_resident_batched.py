@@ -228,3 +228,60 @@ def iteration_cases():
         return [(X[i], p[i], 1000, 1e-5) for i in range(4)]
     cases.append(("strided", strided))
     return cases
+
+
+@pytest.mark.parametrize("case", ["batched_prenoise", "single_panels_prenoise", "c2_rows_gm"])
+def test_checkin_failure_streams_with_x_untouched(monkeypatch, case):
+    """A resident grid that is not co-resident fails its check-in (device_util.h
+    grid_checkin) before any block reads or writes X, within 100 ms instead of an
+    iteration's 2 s poll: the call streams — the
+    fused pre-noise then lands exactly once, as OMA's draws — and the context streams
+    the next calls straight away.  GMAGG_RES_CHECKIN_FAIL=1 makes the check-in wait for
+    a block that does not exist."""
+    import time
+
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd.batched import ProblemPanels, gm2_batched, oma_batched
+    bz.aggregators.close_all()                       # a fresh context (no skip state)
+    X, p = _problems(4, 50, 30_000 if case == "batched_prenoise" else 7850, seed=71)
+    X, p = X.cuda(), p.cuda()
+    if case == "batched_prenoise":
+        want_x = oma_batched(X.clone(), 1e-2, seed=5)
+        want, _ = gm2_batched(want_x, {"maxiter": 1000, "guess": p, "algo": "stream"})
+        A = X.clone()
+        run = lambda: gm2_batched(A, {"maxiter": 1000, "guess": p, "pre_oma_var": 1e-2,  # noqa: E731
+                                      "pre_oma_seed": 5})
+    elif case == "single_panels_prenoise":
+        ref = X[0].clone()
+        bz.OMA(ref, 1e-2, seed=5)
+        want_x = bz.ClientPanels.from_rows(ref).data
+        want = bz.gm2(ref, {"maxiter": 1000, "guess": p[0], "algo": "stream"})
+        A = bz.ClientPanels.from_rows(X[0])
+        run = lambda: (bz.gm2(A, {"maxiter": 1000, "guess": p[0], "pre_oma_var": 1e-2,  # noqa: E731
+                                  "pre_oma_seed": 5}), [bz.aggregators.last_result])
+    else:
+        opts = {"maxiter": 200, "guess": p[0], "noise_var": 1e-2, "seed": 9}
+        want = bz.gm(X[0], dict(opts, algo="stream"))
+        want_x, A = X[0].clone(), X[0]
+        run = lambda: (bz.gm(A, dict(opts)), [bz.aggregators.last_result])  # noqa: E731
+    # AUTO takes the resident kernel on this shape when the check-in passes
+    _, res_ok = run() if case == "c2_rows_gm" else (None, None)
+    if case == "c2_rows_gm":
+        assert res_ok[0].algo == "resident"
+    monkeypatch.setenv("GMAGG_RES_CHECKIN_FAIL", "1")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    got, res = run()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    monkeypatch.delenv("GMAGG_RES_CHECKIN_FAIL")
+    assert all(r.algo == "stream" for r in res), res
+    assert dt < 1.5, dt                              # one 100 ms check-in, not a 2 s poll
+    got_x = A.data if case == "single_panels_prenoise" else A
+    assert torch.equal(got_x, want_x)                # noised exactly once (or untouched)
+    assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-5
+    # the context remembers: the next call streams without trying the resident kernel
+    if case == "c2_rows_gm":
+        run()
+        assert bz.aggregators.last_result.algo == "stream"
+    bz.aggregators.close_all()

@@ -140,3 +140,8 @@ def test_shard_alignment_rule():
     assert not _aligned([(0, 1001)], 2000)              # hi not a multiple of 4
     assert not _aligned([(100, 512)], 2000)             # lo not 256-aligned
     assert _aligned([(0, 1001)], 1001)                  # ragged end of the update
+    # world > 1: the shards must tile [0, d_total)
+    assert not _aligned([(0, 1024), (768, 2000)], 2000)  # overlap
+    assert not _aligned([(0, 768), (1024, 2000)], 2000)  # gap
+    assert not _aligned([(0, 1024), (1024, 1536)], 2000)  # short of d_total
+    assert _aligned([(1024, 2000), (0, 1024)], 2000)     # any rank order

@@ -136,3 +136,19 @@ def test_sgd_counterpart_bit_exact_more_attacks(attack, var, name):
     assert tl == meta["trainLossPath"] and vl == meta["valLossPath"]
     assert ta == meta["trainAccPath"] and vacc == meta["valAccPath"]
     assert [float(v) for v in vv] == meta["variencePath"]
+
+
+def test_client_kernel_rejects_mismatched_dataset():
+    """The fused client kernel (clients.hip) reads F features per sample and trains on
+    labels in [0, C): a dataset that the per-client torch loop would reject must not
+    reach it — _ClientChain._unsupported names the mismatch."""
+    from byzantine_aircomp_amd.training import MLP, _ClientChain
+    model = MLP(784, 10)
+    loss = torch.nn.CrossEntropyLoss()
+    ok = torch.utils.data.TensorDataset(torch.zeros(8, 28, 28), torch.arange(8) % 10)
+    assert _ClientChain._unsupported(model, loss, ok, 4, 10) is None
+    wide = torch.utils.data.TensorDataset(torch.zeros(8, 29, 28), torch.arange(8) % 10)
+    assert "features" in _ClientChain._unsupported(model, loss, wide, 4, 10)
+    for y in (torch.arange(8) + 5, torch.arange(8) - 1, torch.zeros(8)):
+        bad = torch.utils.data.TensorDataset(torch.zeros(8, 28, 28), y)
+        assert "labels" in _ClientChain._unsupported(model, loss, bad, 4, 10)
