@@ -104,6 +104,13 @@ def parse():
     p.add_argument("--reading", default="prenoise", choices=["prenoise", "aircomp"],
                    help="c5: var > 0 as the reference's `--agg gm2 --var v` (OMA pre-noise, then "
                         "gm2; M:351-353) or as the AirComp gm aggregator (M:131-160)")
+    p.add_argument("--c5-recipe", default=None, choices=["outlier", "caller"],
+                   help="c5 data: 'outlier' = honest N(0,0.05^2), B rows N(0.25,0.5^2), guess "
+                        "N(0,0.01^2); 'caller' = the reference's own caller (M:349: the guess is "
+                        "the current model p ~ N(0,0.07^2), honest rows p + N(0,(5e-4)^2), B rows "
+                        "p + 2e-3 + N(0,(5e-3)^2)).  Default: outlier for the prenoise reading, "
+                        "caller for the aircomp reading (on the outlier data the reference's own "
+                        "gm diverges to NaN; DESIGN.md §3.6)")
     p.add_argument("--one-gpu", action="store_true",
                    help="N>1 rehearsal on a one-GPU box: every rank on cuda:0, gloo process "
                         "group, the torch all-reduce callback instead of RCCL (timing is not "
@@ -282,24 +289,35 @@ def run_c5(args, json_out, rank=0, world=1):
                            torch.empty(P, d, device=dev),
                            ProblemPanels(P, K, d, device=dev) if use_panels else None))
 
-    def fill_problem(vi, c0, p, dst):
-        B = C5_BYZ[(c0 + p) % 3]
-        _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, dst.data_ptr(), K, d, d, B, 0.0,
-                                               0.05, 0.25, 0.5, rs + 1000 * vi + c0 + p,
-                                               stream), "fill")
+    def recipe_of(reading):
+        return args.c5_recipe or ("caller" if reading == "aircomp" else "outlier")
 
-    def fill():
+    def fill_problem(vi, c0, p, dst, g0p, recipe):
+        """Problem p's [K, d] rows into dst (its guess g0p already filled)."""
+        B = C5_BYZ[(c0 + p) % 3]
+        seed = rs + 1000 * vi + c0 + p
+        if recipe == "outlier":
+            _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, dst.data_ptr(), K, d, d, B, 0.0,
+                                                   0.05, 0.25, 0.5, seed, stream), "fill")
+        else:      # rows around the current model (the guess): the reference's caller
+            _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, dst.data_ptr(), K, d, d, B, 0.0,
+                                                   5e-4, 2e-3, 5e-3, seed, stream), "fill")
+            dst += g0p
+
+    def fill(reading):
+        recipe = recipe_of(reading)
         for vi, var, c0, X, g0, Pn in groups:
+            _lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), g0.numel(), 0.0,
+                                                  0.01 if recipe == "outlier" else 0.07,
+                                                  rs + 777 + vi + c0, stream), "fill")
             for p in range(g0.shape[0]):
                 if Pn is None:
-                    fill_problem(vi, c0, p, X[p])
+                    fill_problem(vi, c0, p, X[p], g0[p], recipe)
                 else:
-                    fill_problem(vi, c0, p, tmp)
+                    fill_problem(vi, c0, p, tmp, g0[p], recipe)
                     _lib.check(ctx.lib.gm_rows_to_panels_f32(
                         ctx.handle, tmp.data_ptr(), K, d, d, Pn.data[p].data_ptr(), Pn.W,
                         Pn.panel_stride, stream), "pack")
-            _lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), g0.numel(), 0.0, 0.01,
-                                                  rs + 777 + vi + c0, stream), "fill")
         torch.cuda.synchronize(dev)
 
     outs = {}                        # the last step's aggregates per group (for `check`)
@@ -334,11 +352,11 @@ def run_c5(args, json_out, rank=0, world=1):
 
     def measure(reading, steps, warmup):
         for _ in range(warmup):
-            fill()
+            fill(reading)
             step(reading)
         total, pass_ms, launches, iters, groups_out = 0.0, 0.0, 0, [], {}
         for _ in range(steps):
-            fill()
+            fill(reading)
             ctx.pass_timing(True)
             torch.cuda.synchronize(dev)
             if dist is not None:
@@ -358,7 +376,8 @@ def run_c5(args, json_out, rank=0, world=1):
         return total, pass_ms, launches, iters, groups_out
 
     total, pass_ms, launches, iters, per_group = measure(args.reading, args.steps, args.warmup)
-    check = c5_check(groups, outs, args.reading) if not args.no_check else None
+    check = c5_check(groups, outs, args.reading, args.maxiter, recipe_of(args.reading)) \
+        if not args.no_check else None
     n_prob = len(iters)
     mean_it = sum(iters) / n_prob
     step_bytes = sum(iters) * 4.0 * K * d            # algorithmic STEP-pass bytes per sweep
@@ -368,7 +387,8 @@ def run_c5(args, json_out, rank=0, world=1):
     alt = None
     if args.alt_steps != 0 and world == 1:
         a_total, _, _, a_iters, a_groups = measure(alt_reading, 1, 0)
-        alt = {"reading": alt_reading, "value": len(a_iters) / a_total, "seconds": a_total,
+        alt = {"reading": alt_reading, "recipe": recipe_of(alt_reading),
+               "value": len(a_iters) / a_total, "seconds": a_total,
                "mean_iters": sum(a_iters) / len(a_iters),
                "groups": {str(k): {"problems_per_s": v["problems"] / v["seconds"],
                                    "mean_iters": v["iters"] / v["problems"]}
@@ -427,7 +447,7 @@ def run_c5(args, json_out, rank=0, world=1):
     if not args.no_cpu and world == 1:
         vi0, _, c00, X0, g00, _ = groups[0]
         if X0 is None:                       # problem 0's clean rows, regenerated
-            fill_problem(vi0, c00, 0, tmp)
+            fill_problem(vi0, c00, 0, tmp, g00[0], recipe_of(args.reading))
             torch.cuda.synchronize(dev)
         cpu = c5_cpu_baseline(tmp if X0 is None else X0[0], g00[0], mean_it, n_prob,
                               args.cpu_budget)
@@ -436,8 +456,10 @@ def run_c5(args, json_out, rank=0, world=1):
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": 1e3 * total / args.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic (Philox on device: honest N(0,0.05^2), B rows N(0.25,0.5^2), "
-                "guess N(0,0.01^2))",
+        "data": ("synthetic (Philox on device: honest N(0,0.05^2), B rows N(0.25,0.5^2), "
+                 "guess N(0,0.01^2))" if recipe_of(args.reading) == "outlier" else
+                 "synthetic (Philox on device, the reference's caller M:349: guess = model p ~ "
+                 "N(0,0.07^2), honest rows p + N(0,(5e-4)^2), B rows p + 2e-3 + N(0,(5e-3)^2))"),
         "config": {"workload": f"c5: {n_prob} independent gm2 problems K={K} x d={d} fp32 over "
                                f"var {list(C5_VARS)} x B {list(C5_BYZ)}, reading '{args.reading}'"
                                + ((" (OMA pre-noise then gm2, M:351-353; separate OMA pass)"
@@ -446,7 +468,7 @@ def run_c5(args, json_out, rank=0, world=1):
                                    "into gm2's first pass)")
                                   if args.reading == "prenoise" else " (AirComp gm for var > 0)"),
                    "K": K, "d": d, "problems": n_prob, "mean_iters": mean_it, "batch": chunk,
-                   "algo": algo_used,
+                   "algo": algo_used, "recipe": recipe_of(args.reading),
                    "parallelism": ("register-resident batched (one launch per group: each problem "
                                    "held on chip for all its iterations)" if algo_used == "resident"
                                    else "batched (one launch per pass covers every problem of a group)")
@@ -464,21 +486,43 @@ def run_c5(args, json_out, rank=0, world=1):
     print(json.dumps(line), file=json_out, flush=True)
 
 
-def c5_check(groups, outs, reading, per_group=3):
-    """Full-size correctness of the last timed sweep: for the first, middle and last
-    problem of every group, the fp64 gm2 fixed-point step ||T(g) - g|| (T = M:174-179)
-    at the returned aggregate, over that problem's (noisy, for the prenoise reading)
-    K x d matrix as the kernels read it.  The reference stops at movement <= tol = 1e-5;
-    a wrong aggregate shows up as a large step.  (AirComp gm groups never converge:
-    their problems are checked for finite output only.)"""
-    worst, worst_rel, n, finite = 0.0, 0.0, 0, True
+def c5_check(groups, outs, reading, maxiter, recipe, per_group=3):
+    """Full-size correctness of the last timed sweep.
+
+    gm2 groups (var = 0, and every group of the prenoise reading): for the first, middle
+    and last problem, the fp64 gm2 fixed-point step ||T(g) - g|| (T = M:174-179) at the
+    returned aggregate over that problem's (noisy, for the prenoise reading) K x d matrix
+    as the kernels read it; the reference stops at movement <= tol = 1e-5, a wrong
+    aggregate shows up as a large step.
+
+    AirComp gm groups (never converge, 1000 iterations): the fraction of problems with a
+    finite aggregate, and the distance of each aggregate from the ideal GM of the same
+    problem (gm2_batched, untimed) — the AirComp error a draw.ipynb-style sweep plots.
+    The reference's own gm is unstable once sqrt(var d / 2) exceeds K / (sqrt(500) s)
+    (s = RMS of the iterate; its noise then outgrows the distances that scale the signal,
+    DESIGN.md §3.6): at d = 100k, s = 0.07 that is var ~ 0.02, so the var = 0.1 group
+    diverges in the reference too (tests/test_oracle_c5_stability.py); `ok` requires
+    finite aggregates in the groups below the bound only.  The kernel is pinned to
+    oracle.gm over 1000 iterations by tests/test_gpu_c5_fullsize.py."""
+    from byzantine_aircomp_amd.batched import gm2_batched
+    worst, worst_rel, n, ok_air = 0.0, 0.0, 0, True
+    air = {}
     for vi, var, c0, Xr, g0, Pn in groups:
         out, res = outs[(vi, c0)]
         P = out.shape[0]
+        if reading == "aircomp" and var > 0:
+            X = Pn if Pn is not None else Xr
+            ideal, _ = gm2_batched(X, {"maxiter": maxiter, "tol": 1e-5, "guess": g0})
+            fin = torch.isfinite(out).all(dim=1)
+            rel = ((out - ideal).norm(dim=1) / ideal.norm(dim=1))[fin]
+            a = air.setdefault(str(var), {"problems": 0, "finite": 0, "rel_to_gm2": []})
+            a["problems"] += P
+            a["finite"] += int(fin.sum())
+            a["rel_to_gm2"] += rel.tolist()
+            if recipe == "outlier" or _c5_stable(var, X):
+                ok_air &= bool(fin.all())
+            continue
         for p in sorted({0, P // 2, P - 1})[:per_group]:
-            if reading == "aircomp" and var > 0:
-                finite &= bool(torch.isfinite(out[p]).all())
-                continue
             if Pn is not None:
                 Xp = Pn.data[p].permute(1, 0, 2).reshape(Pn.K, Pn.npan * Pn.W)[:, :Pn.d]
             else:
@@ -487,11 +531,32 @@ def c5_check(groups, outs, reading, per_group=3):
             worst = max(worst, step)
             worst_rel = max(worst_rel, step / max(gn, 1e-300))
             n += 1
-    return {"what": "fp64 gm2 step ||T(g) - g|| / ||g|| at the returned g of the first, middle "
-                    "and last problem of every group, over the problem's full K x d matrix "
-                    "(noisy for the prenoise reading); T = M:174-179",
-            "problems_checked": n, "max_fixed_point_step": worst, "max_relative_step": worst_rel,
-            "finite": finite, "ok": finite and worst <= 1e-4}
+    out = {"what": "gm2 groups: fp64 gm2 step ||T(g) - g|| / ||g|| at the returned g of the "
+                   "first, middle and last problem of every group, over the problem's full K x d "
+                   "matrix (noisy for the prenoise reading); T = M:174-179",
+           "problems_checked": n, "max_fixed_point_step": worst, "max_relative_step": worst_rel,
+           "ok": ok_air and worst <= 1e-4}
+    if air:
+        out["aircomp_groups"] = {
+            k: {"finite_frac": v["finite"] / v["problems"],
+                "mean_rel_to_gm2": (sum(v["rel_to_gm2"]) / len(v["rel_to_gm2"])
+                                    if v["rel_to_gm2"] else None),
+                "max_rel_to_gm2": max(v["rel_to_gm2"]) if v["rel_to_gm2"] else None,
+                "below_stability_bound": recipe == "caller" and _c5_stable(float(k), groups[0][5]
+                                                                           or groups[0][3])}
+            for k, v in air.items()}
+        out["aircomp_what"] = ("AirComp gm groups: finite fraction over every problem, and "
+                               "||g_gm - g_gm2|| / ||g_gm2|| against the ideal GM of the same problem; "
+                               "the reference's gm is unstable above var ~ 0.02 at d = 100k "
+                               "(sqrt(var d / 2) > K / (sqrt(500) s), s = 0.07)")
+    return out
+
+
+def _c5_stable(var, X, s=0.07):
+    """The caller recipe's stability bound for the reference's gm: sqrt(var d / 2) below
+    K / (sqrt(500) s) (s = the model's RMS, 0.07)."""
+    K, d = (X.shape[1], X.shape[2]) if isinstance(X, torch.Tensor) else (X.K, X.d)
+    return math.sqrt(var * d / 2) < K / (math.sqrt(500.0) * s)
 
 
 def c5_cpu_baseline(X, g0, mean_iters, problems, budget):

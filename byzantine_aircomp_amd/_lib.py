@@ -19,7 +19,7 @@ GM_NOISE_PHILOX, GM_NOISE_HOST = 0, 1
 GM_ALGO_AUTO, GM_ALGO_STREAM, GM_ALGO_TWOPASS, GM_ALGO_GRAM, GM_ALGO_RESIDENT = 0, 1, 2, 3, 4
 GM_ALGO_GRAM_F32 = 5
 GM_LAYOUT_ROWS, GM_LAYOUT_PANELS = 0, 1
-GM_GUARD_NONE, GM_GUARD_ACCEPTED, GM_GUARD_REJECTED = 0, 1, 2
+GM_GUARD_NONE, GM_GUARD_ACCEPTED, GM_GUARD_REJECTED, GM_GUARD_ACCEPTED_FLOOR = 0, 1, 2, 3
 
 NOISE_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.POINTER(C.c_float),
                        C.POINTER(C.c_float), C.POINTER(C.c_float))

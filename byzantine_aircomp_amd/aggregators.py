@@ -56,7 +56,7 @@ class GMResult:
     last_movement: float
     converged: bool
     algo: str
-    guard: str = "none"      # Gram accuracy guard: "none", "accepted", "rejected"
+    guard: str = "none"      # Gram guard: "none", "accepted", "accepted_floor", "rejected"
     gram_kind: str = ""      # Gram runs: "f16_split", "bf16_split" (f16 range fallback), "f32"
 
 
@@ -66,7 +66,7 @@ _ALGOS = {"auto": _lib.GM_ALGO_AUTO, "stream": _lib.GM_ALGO_STREAM,
           "resident": _lib.GM_ALGO_RESIDENT, "gram_f32": _lib.GM_ALGO_GRAM_F32}
 _ALGO_NAMES = {v: k for k, v in _ALGOS.items()}
 _GUARD_NAMES = {_lib.GM_GUARD_NONE: "none", _lib.GM_GUARD_ACCEPTED: "accepted",
-                _lib.GM_GUARD_REJECTED: "rejected"}
+                _lib.GM_GUARD_REJECTED: "rejected", _lib.GM_GUARD_ACCEPTED_FLOOR: "accepted_floor"}
 
 
 def _result(res) -> "GMResult":

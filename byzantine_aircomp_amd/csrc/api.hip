@@ -479,9 +479,13 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
 // those with the K-space map's and measures the one-step error e = ||X'^T b||.
 // The result is kept only if (1) e / (1 - rho) <= 1e-6 ||g|| (rho = the last
 // K-space contraction ratio, clamped to [0.5, 0.95]), and (2) the reference's own
-// movement noise floor, measured at 0.4-1.8 x 2^-24 ||g||, is
-// below tol/3, so that the reference stops within +-1 iteration of the exact
-// loop.  Otherwise *rejected is set and the caller runs the streaming path.
+// fp32 movement noise floor, measured at 0.4-1.8 x 2^-24 ||g|| and
+// taken as 2^-23 ||g||, is at most tol, so that the reference's loop does stop.
+// Otherwise *rejected is set and the caller runs the streaming path.  With the floor
+// below tol/3 the reference stops within +-1 iteration of the exact loop (guard
+// ACCEPTED); between tol/3 and tol its count is decided by rounding — the streaming
+// path's too — and the Gram's exact count lies in that window of legitimate stopping
+// points (guard ACCEPTED_FLOOR; round 4: the whole C4 job, ||g|| = 74, is here).
 int run_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, const float* guess0,
              float* out, const gm_opts* o, gm_result* res, const PassCfg& cfg, hipStream_t s,
              bool split, bool guarded, bool* rejected, int64_t pstride = 0) {
@@ -562,6 +566,7 @@ again:
     gg = gb;
     goto again;
   }
+  bool floor_band = false;
   if (guarded) {
     const double u = std::ldexp(1.0, -24);
     const double gn = std::sqrt(std::max(0.0, hsums[1]));
@@ -569,12 +574,15 @@ again:
     rho = rho != rho ? 0.5 : std::min(0.95, std::max(0.5, rho));
     const double pred = hst->guard_q / (1.0 - rho) / gn;
     const bool accurate = pred <= 1e-6;                     // NaN fails
-    const bool floor_ok = !hst->converged || 2.0 * u * gn <= o->tol / 3.0;
+    const double floor = 2.0 * u * gn;
+    const bool floor_ok = !hst->converged || floor <= o->tol;
+    floor_band = hst->converged && floor > o->tol / 3.0;
     static const bool dbg = getenv("GMAGG_GUARD_DEBUG") != nullptr;
     if (dbg)
       fprintf(stderr, "[gram guard] K=%lld d=%lld q=%.3e rho=%.3f |g|=%.4e pred=%.3e converged=%d "
-              "iters=%d floor_ok=%d accurate=%d\n", (long long)K, (long long)d, hst->guard_q, rho,
-              gn, pred, (int)hst->converged, (int)hst->iters, (int)floor_ok, (int)accurate);
+              "iters=%d floor_ok=%d band=%d accurate=%d\n", (long long)K, (long long)d, hst->guard_q,
+              rho, gn, pred, (int)hst->converged, (int)hst->iters, (int)floor_ok, (int)floor_band,
+              (int)accurate);
     if (!accurate || !floor_ok) {
       *rejected = true;
       return GM_OK;
@@ -586,7 +594,7 @@ again:
   r.converged = hst->converged;
   r.algo_used = split ? GM_ALGO_GRAM : GM_ALGO_GRAM_F32;
   r.gram_kind = kind == GramKind::H16 ? 1 : kind == GramKind::BF16 ? 2 : 3;
-  r.guard = guarded ? GM_GUARD_ACCEPTED : GM_GUARD_NONE;
+  r.guard = !guarded ? GM_GUARD_NONE : floor_band ? GM_GUARD_ACCEPTED_FLOOR : GM_GUARD_ACCEPTED;
   if (res) *res = r;
   return GM_OK;
 }

@@ -120,7 +120,10 @@ typedef struct gm_opts {
 enum gm_guard {
     GM_GUARD_NONE = 0,        /* no Gram result was involved */
     GM_GUARD_ACCEPTED = 1,    /* Gram-space result, a-posteriori accuracy guard passed */
-    GM_GUARD_REJECTED = 2     /* a Gram result was refused; the streaming path produced out */
+    GM_GUARD_REJECTED = 2,    /* a Gram result was refused; the streaming path produced out */
+    GM_GUARD_ACCEPTED_FLOOR = 3 /* accepted, with tol inside the reference's fp32 movement
+                                 floor band (tol/3 < 2^-23 ||g|| <= tol): any fp32 Weiszfeld's
+                                 count is decided by rounding there; iters is the exact count */
 };
 
 typedef struct gm_result {

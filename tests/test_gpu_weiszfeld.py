@@ -411,6 +411,36 @@ def _guard_data(case):
     return X, torch.zeros(d)
 
 
+@pytest.mark.parametrize("shift", [0.0, 0.07])
+def test_gram_c4_recipe_vs_oracle(shift):
+    """north_star's second design on the C4 recipe (K = 256, d = 2^20), AUTO, against the
+    oracle gm2.  shift = 0: ||g|| ~ 6.8, the fp32 movement floor (2^-23 ||g||) far below
+    tol/3: guard 'accepted', iterations +-1.  shift = 0.07 (every element and the guess;
+    the algorithm is translation-invariant, the rounding is not): ||g|| ~ 72, the floor
+    8.6e-6 between tol/3 and tol — the whole C4 job's regime (||g|| = 74 at d = 125M):
+    guard 'accepted_floor', the count checked against the window of counts an fp32
+    Weiszfeld may stop at (oracle.gm2_count_window), the aggregate to 1e-5 of both the
+    oracle and the streaming path."""
+    m = bz()
+    X, g0 = _c4_like(256, 1 << 20, seed=4040)
+    X += shift
+    g0 += shift
+    got = m.gm2(X, {"maxiter": 1000, "guess": g0})
+    res = m.aggregators.last_result
+    assert res.algo == "gram"
+    assert res.guard == ("accepted" if shift == 0.0 else "accepted_floor"), res
+    Xc, gc = X.cpu(), g0.cpu()
+    want, tr = orc.gm2(Xc, {"maxiter": 1000, "tol": 1e-5, "guess": gc.clone()})
+    assert rel_l2(got.cpu().numpy(), want.numpy()) <= TOL
+    window = orc.gm2_count_window(Xc, gc, 1000, 1e-5) if shift else None
+    assert_iter_count(res.iters, tr.iters, window)
+    if shift:
+        # the C4 regime is rounding-determined: the window is wider than +-1
+        assert window.width > 1
+    s = m.gm2(X, {"maxiter": 1000, "guess": g0, "algo": "stream"})
+    assert rel_l2(got.cpu().numpy(), s.cpu().numpy()) <= TOL
+
+
 @pytest.mark.parametrize("case", GUARD_CASES)
 def test_gram_guard_falls_back_to_streaming(case):
     """Data where the Gram may not reproduce the reference: the reference's fp32
