@@ -71,6 +71,8 @@ def parse():
     p.add_argument("--var", type=float, default=None,
                    help="gm noise variance (default: the workload's; None = no AWGN)")
     p.add_argument("--maxiter", type=int, default=1000)
+    p.add_argument("--tol", type=float, default=1e-5,
+                   help="the reference's tol (1e-5); < 0 runs maxiter iterations (probes only)")
     p.add_argument("--layout", default="auto", choices=["auto", "rows", "panels"],
                    help="client matrix layout: rows = the reference's [K, d] stack; panels = "
                         "ClientPanels [ceil(d/W)][K][W] (streaming algorithm); auto = panels "
@@ -142,8 +144,9 @@ def pmc_traffic(workload, layout, kernel="weiszfeld_pass", mode="0"):
     and layout; tools/pmc_summary.py applies the gfx950 FETCH_SIZE x2 correction)."""
     import glob
     import re
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}*.json")))
-    for path in reversed(files):
+    files = [f for f in glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}_*.json"))]
+    files += glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}.json"))
+    for path in sorted(files, key=profile_order, reverse=True):
         data = json.load(open(path))
         for name, row in data["kernels"].items():
             if kernel == "weiszfeld_pass":
@@ -162,6 +165,38 @@ def pmc_traffic(workload, layout, kernel="weiszfeld_pass", mode="0"):
             elif kernel in name:
                 return row["hbm_bytes_per_launch"] / 1e9, os.path.relpath(path, ROOT)
     return None, None
+
+
+def latency_floor(kernel):
+    """The newest profiles/r*_latency_floor.json entry for a register-resident kernel
+    (its exchange-only time per iteration, measured with the compute phases skipped)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_latency_floor.json")),
+                   key=profile_order, reverse=True)
+    for path in files:
+        data = json.load(open(path))
+        if kernel in data:
+            return data[kernel], os.path.relpath(path, ROOT)
+    return None, None
+
+
+def profile_order(path):
+    """(round, session, suffix) of a profiles/ file name: r0N_* = round 1 session N,
+    r2_* / r2a_* / r2b_* ... = round 2 sessions 0 / 1 / 2 ..., r3s2z_* = round 3 session 2
+    variant z, r4s1_* = round 4 session 1 — the newest measurement wins, whatever the
+    lexical order of the names."""
+    import re
+    name = os.path.basename(path).split("_")[0]
+    m = re.fullmatch(r"r0(\d)", name)
+    if m:
+        return (1, int(m.group(1)), "")
+    m = re.fullmatch(r"r(\d+)s(\d+)([a-z]*)", name)
+    if m:
+        return (int(m.group(1)), int(m.group(2)), m.group(3))
+    m = re.fullmatch(r"r(\d+)([a-z]?)", name)
+    if m:
+        return (int(m.group(1)), (ord(m.group(2)) - ord("a") + 1) if m.group(2) else 0, "")
+    return (0, 0, name)
 
 
 def columns(src, c0, c1):
@@ -326,7 +361,7 @@ def run_c5(args, json_out, rank=0, world=1):
         iters, per_group = [], {}
         for vi, var, c0, Xr, g0, Pn in groups:
             X = Pn if Pn is not None else Xr
-            opts = {"maxiter": args.maxiter, "tol": 1e-5, "guess": g0}
+            opts = {"maxiter": args.maxiter, "tol": args.tol, "guess": g0}
             t0 = time.perf_counter()
             if var == 0.0:
                 out, res = gm2_batched(X, opts)
@@ -410,23 +445,45 @@ def run_c5(args, json_out, rank=0, world=1):
                                 if args.reading == "prenoise" else
                                 (None, "no PMC pass on record for the aircomp reading"))
         achieved = hbm_bytes * args.steps / (pass_ms / 1e3) / 1e9 if pass_ms > 0 else None
+        # The kernel is latency-bound: each iteration is a cross-CU exchange of every block's
+        # partials plus the phases' VALU work, with the problem's tile on chip.  Roofline =
+        # time per iteration of one problem in flight (a group of NB blocks) against the
+        # exchange floor (the same kernel with its compute phases skipped; profiles/),
+        # the tile load's fixed cost per problem (profiled) taken out first.
+        fl, fl_src = latency_floor("weiszfeld_resident_batched")
+        ng = fl["groups"] if fl else None
+        it_us = None
+        if fl and pass_ms > 0:
+            probs = len(iters)
+            t_step_us = 1e3 * pass_ms / args.steps
+            it_us = (t_step_us * ng / probs - fl["fixed_us_per_problem"]) / (sum(iters) / probs)
         roofline = {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
-            "traffic_unit": "GB per launch (one 1024-problem group, PMC)",
-            "traffic_algorithmic": per_launch / 1e9, "traffic_source": traffic_src,
+            "bound": "latency", "unit": "us per iteration (one problem in flight)",
+            "achieved": it_us, "peak": fl["exchange_floor_us_per_iteration"] if fl else None,
+            "frac": fl["exchange_floor_us_per_iteration"] / it_us if fl and it_us else None,
+            "frac_def": "exchange floor / achieved time per iteration (<= 1; time-like: the floor "
+                        "is the fastest an iteration can be with this exchange)",
+            "floor_source": fl_src,
+            "achieved_def": "(summed kernel time per sweep x groups / problems - the profiled fixed "
+                            "cost per problem: tile load, INIT, last gather) / mean iterations",
             "kernel": "weiszfeld_resident_batched (each problem's X read once, held in VGPRs + "
                       "LDS for all its iterations)",
             "launches_timed": launches, "avg_launch_us": 1e3 * pass_ms / max(launches, 1),
-            "algorithmic_bytes": "4*K*d per problem (one read of X) + 4*K*d per problem of the "
-                                 "prenoise groups (the noised X written back), / summed kernel time",
-            "streaming_equivalent_GBs": step_bytes * args.steps / (pass_ms / 1e3) / 1e9
-            if pass_ms > 0 else None,
-            "streaming_equivalent_def": "sum_p 4*K*d*iters_p (the streaming path's STEP-pass "
-                                        "bytes) / summed kernel time",
-            "aggregation_frac": agg_bytes / (total / args.steps) / 1e9 / HBM_PEAK_GBS,
-            "aggregation_frac_def": "sum_p 4*K*d*(iters_p+1) / ms_per_step / 8 TB/s: the "
-                                    "streaming algorithm's bytes over the sweep's time"}
+            "traffic": traffic, "traffic_unit": "GB per launch (one 1024-problem group, PMC)",
+            "traffic_algorithmic": per_launch / 1e9, "traffic_source": traffic_src,
+            "hbm_tile_load": {
+                "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                "achieved": fl.get("tile_load_hbm_GBs") if fl else None,
+                "frac": fl["tile_load_hbm_GBs"] / HBM_PEAK_GBS if fl else None,
+                "source": fl.get("tile_load_note") if fl else None,
+                "kernel_bytes_over_kernel_time_GBs": achieved,
+                "kernel_bytes_def": "4*K*d per problem (one read of X) + 4*K*d per problem of the "
+                                    "prenoise groups (the noised X written back), / summed kernel "
+                                    "time (iterations included: not an HBM rate of the loads)"},
+            "streaming_equivalent_frac": agg_bytes / (total / args.steps) / 1e9 / HBM_PEAK_GBS,
+            "streaming_equivalent_def": "sum_p 4*K*d*(iters_p+1) / ms_per_step / 8 TB/s: the bytes "
+                                        "the streaming path would move, over the sweep's time (a "
+                                        "comparison with streaming, not a roofline)"}
     else:
         traffic, traffic_src = pmc_traffic("c5", "panels" if use_panels else "rows")
         roofline = {
@@ -688,7 +745,7 @@ def main():
     g0 = torch.empty(d, dtype=torch.float32, device=dev)
     _lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), d, 0.0, 0.01, 20212, stream),
                "fill")
-    opts = {"maxiter": args.maxiter, "tol": 1e-5, "guess": g0, "algo": args.algo}
+    opts = {"maxiter": args.maxiter, "tol": args.tol, "guess": g0, "algo": args.algo}
     if agg_name == "gm":
         opts.update(noise_var=var, seed=2021)
     if sg is not None:
@@ -808,7 +865,7 @@ def main():
             hb = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": gbs / HBM_PEAK_GBS, "traffic": traffic}
             roof, other = (mf, hb) if mf["frac"] >= hb["frac"] else (hb, mf)
-            roof.update({"kernel": (f"gram_h16_partial ({layout}; v_mfma_f32_32x32x16_f16 x3, "
+            roof.update({"kernel": (f"gram_h16_partial ({layout}; v_mfma_f32_16x16x32_f16, 3 products, "
                                     "scaled h+m split, upper-triangle tiles)") if h16 else
                                    ("gram_split_partial (v_mfma_f32_32x32x16_bf16 x4, h+m split, "
                                     "upper-triangle tiles)") if split else
@@ -823,21 +880,27 @@ def main():
                          "aggregation_frac_def": "2 reads of X (Gram + closing pass) x 4*K*d_local "
                                                  "/ ms_per_step / 8 TB/s"})
         elif res.algo == "resident":
-            # one cooperative launch runs the whole aggregation with X held in VGPRs
-            # (resident.hip): price its algorithmic bytes as 4*K*d per pass over the
-            # iterations it ran; the matrix (1.57 MB at C2) lives in registers, so this is a
-            # latency-bound kernel and the HBM fraction says how far from streaming it is
-            bytes_agg = per_launch_bytes * passes
-            gbs = bytes_agg / avg_pass_s / 1e9
-            roof = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": gbs / HBM_PEAK_GBS, "traffic": None,
-                    "kernel": "weiszfeld_resident (every iteration in one cooperative launch)",
+            # one launch runs the whole aggregation with X held in VGPRs (resident.hip, or
+            # for panels the batched kernel with P = 1): X (1.57 MB at C2) is read once, so
+            # the kernel is latency-bound — each iteration is a cross-CU exchange of every
+            # block's partials plus the phases' VALU work.  Roofline: time per iteration
+            # against the exchange floor (the kernel with its compute phases skipped, profiles/)
+            us_it = avg_pass_s * 1e6 / max(res.iters, 1)
+            fl, fl_src = latency_floor("weiszfeld_resident" if layout == "rows"
+                                       else "weiszfeld_resident_batched")
+            floor = fl["exchange_floor_us_per_iteration"] if fl else None
+            roof = {"bound": "latency", "unit": "us per iteration", "achieved": us_it,
+                    "peak": floor, "frac": floor / us_it if floor else None,
+                    "frac_def": "exchange floor / achieved time per iteration (<= 1)",
+                    "floor_source": fl_src, "traffic": None,
+                    "kernel": "weiszfeld_resident (every iteration in one launch, X in VGPRs)"
+                              if layout == "rows" else "weiszfeld_resident_batched (P = 1)",
                     "launches_timed": launches, "avg_launch_us": avg_pass_s * 1e6,
-                    "us_per_iteration": avg_pass_s * 1e6 / max(res.iters, 1),
-                    "algorithmic_bytes_per_launch": bytes_agg,
-                    "aggregation_frac": agg_frac,
-                    "note": "X (K*d*4 bytes) is read from HBM once per launch and kept in "
-                            "registers; the per-iteration cost is the grid barrier + K-space step"}
+                    "us_per_iteration": us_it,
+                    "streaming_equivalent_frac": agg_frac,
+                    "streaming_equivalent_def": "4*K*d*(iters+1) / ms_per_step / 8 TB/s: the bytes "
+                                                "the streaming path would move (a comparison, not "
+                                                "a roofline: X is read from HBM once per launch)"}
         else:
             traffic, traffic_src = pmc_traffic(args.workload, layout) if world == 1 \
                 else (None, None)

@@ -60,6 +60,14 @@ namespace gmk {
 
 constexpr uint64_t kPollTicks = 200000000ull;   // 2 s at the 100 MHz real-time clock
 
+// GMK_RES_DBG (probe builds only; 0 in the product): phases skipped to price the
+// iteration's exchange alone (tools/gpu.sh probe steps, DESIGN.md §4 latency rooflines):
+// 1 phase B's row sums, 2 the K-space step, 4 phase A's weighted sum.  7 leaves the
+// gather, the barriers and the publish: the exchange floor of the protocol.
+#ifndef GMK_RES_DBG
+#define GMK_RES_DBG 0
+#endif
+
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 
@@ -365,7 +373,9 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
     if (it == a.maxiter) break;
 
     // (3) coefficients for pass `it`: one wave, lane = client, when K <= 64
-    if (K <= 64) {
+    if constexpr ((GMK_RES_DBG & 2) != 0) {
+      if (tid == 0) s_anoise = 0.f;
+    } else if (K <= 64) {
       if (w == 0) {
         const int k = lane;
         const bool kv = k < K;
@@ -455,10 +465,12 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
       float acc[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) acc[v] = 0.f;
+      if constexpr ((GMK_RES_DBG & 4) == 0) {
 #pragma unroll
-      for (int i = 0; i < R; ++i)
+        for (int i = 0; i < R; ++i)
 #pragma unroll
-        for (int v = 0; v < V; ++v) acc[v] = fmaf(wt[i], x[h][i][v], acc[v]);
+          for (int v = 0; v < V; ++v) acc[v] = fmaf(wt[i], x[h][i][v], acc[v]);
+      }
 #pragma unroll
       for (int o = LPR; o < 64; o <<= 1)
 #pragma unroll
@@ -493,7 +505,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
 #pragma unroll
     for (int m = 0; m < RPL; ++m) racc[m] = 0.0;
 #pragma unroll
-    for (int h = 0; h < CPB; ++h) {
+    for (int h = 0; h < CPB && (GMK_RES_DBG & 1) == 0; ++h) {
       float gv[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) gv[v] = s_g[h * J + c * V + v];

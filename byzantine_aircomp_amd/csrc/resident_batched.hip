@@ -141,7 +141,8 @@ __device__ __forceinline__ void rb_all_rows(F f, float* srow, int lane) {
 }  // namespace
 
 // DBG (probe builds, -DGMK_RB_DBG_VARIANTS; 0 in the product): phases skipped to price
-// them (tools/rb_probe.py --dbg): 1 phase B rows, 2 the K-space step, 4 phase A, 8 the
+// them (tools/rb_probe.py --dbg; 7 = the exchange alone, the latency roofline's floor):
+// 1 phase B rows, 2 the K-space step, 4 phase A, 8 the
 // gather's wait for the tags, 16 the publish, 32 the tile load, 64 the INIT rows, 128 the
 // LDS rows' loads, 256 the register rows' loads
 template <int KR, int KV, int MODE, int DBG = 0>
@@ -625,6 +626,7 @@ static const void* rb_kernel(int kr, int mode) {
       case 1: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 1>);
       case 2: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 2>);
       case 4: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 4>);
+      case 7: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 7>);
       case 8: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 8>);
       case 16: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 16>);
       case 31: return reinterpret_cast<const void*>(&weiszfeld_resident_batched<50, 32, 0, 31>);
