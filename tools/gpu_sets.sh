@@ -1,0 +1,228 @@
+#!/bin/bash
+# The GPU-box measurement sets behind profiles/ (one function per set, named by the
+# profile prefix it produced; round 3 kept one script per set under tools/runs/).
+#
+#   bash tools/gpu_sets.sh SET        e.g.  bash tools/gpu_sets.sh r4s1f
+#
+# Every set writes under gpurun_out/, runs each GPU step under its own time limit and
+# stops at the first failing step.  Probe sets that name libgmagg_alt.so need the
+# matching `make alt ALT_FLAGS=...` build first (the flags are in the set's comment).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}" || exit 9
+export TMPDIR=/tmp
+
+r3s2b() {
+  o=gpurun_out/r3s2b; mkdir -p $o
+  timeout -k 10 400 python tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant coop= --variant plain=GMAGG_RES_COOP=0 --out $o/ab_c2_coop.jsonl > $o/ab.log 2>&1 || { tail -20 $o/ab.log; return 1; }
+  tail -2 $o/ab.log
+  GMAGG_RES_COOP=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/c2plain -o t -- python3 bench.py --workload c2 --no-cpu --soak 0 --alt-steps 0 > $o/c2plain.log 2>&1; echo "c2 plain-launch trace return $?"
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $o/probe_plain -o t -- ./tools/coop_exit_probe plain > $o/probe_plain.log 2>&1; echo "probe plain return $?"
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $o/probe_coop -o t -- ./tools/coop_exit_probe coop > $o/probe_coop.log 2>&1; echo "probe coop return $?"
+}
+
+r3s2c() {
+  o=gpurun_out/r3s2c; mkdir -p $o
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_resident_batched.py > $o/t_resident.log 2>&1; rc=$?
+  tail -5 $o/t_resident.log; grep -E "FAILED|Error|assert" $o/t_resident.log | head -20
+  [ $rc -ne 0 ] && return $rc
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_batched.py tests/test_gpu_c5_fullsize.py > $o/t_batched.log 2>&1 || { tail -30 $o/t_batched.log; return 1; }
+  tail -2 $o/t_batched.log
+  timeout -k 10 600 python -u bench.py --workload c5 --no-cpu --alt-steps 0 --soak 0 > $o/c5_res.json 2> $o/c5_res.err || { tail -20 $o/c5_res.err; return 1; }
+  python -c "import json;l=json.load(open('$o/c5_res.json'));print('resident c5', l['value'], l['ms_per_step'], l['check'], l['config']['groups'])"
+  GMAGG_BATCH_RESIDENT=0 timeout -k 10 600 python -u bench.py --workload c5 --no-cpu --alt-steps 0 --soak 0 > $o/c5_stream.json 2> $o/c5_stream.err || { tail -20 $o/c5_stream.err; return 1; }
+  python -c "import json;l=json.load(open('$o/c5_stream.json'));print('stream c5', l['value'], l['ms_per_step'])"
+}
+
+r3s2f() {
+  o=gpurun_out/r3s2f; mkdir -p $o
+  for dbg in 0 1 2 4 8 16 31; do
+    GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so GMAGG_RB_DBG=$dbg timeout -k 10 200 python -u tools/rb_probe.py --quick > $o/dbg$dbg.log 2>&1 || { tail -5 $o/dbg$dbg.log; return 1; }
+    grep fit $o/dbg$dbg.log
+  done
+}
+
+r3s2g() {
+  o=gpurun_out/r3s2g; mkdir -p $o
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_resident_batched.py > $o/t_resident.log 2>&1 || { tail -30 $o/t_resident.log; return 1; }
+  tail -1 $o/t_resident.log
+  for dbg in 0 1 4; do
+    GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so GMAGG_RB_DBG=$dbg timeout -k 10 200 python -u tools/rb_probe.py --quick > $o/dbg$dbg.log 2>&1 || { tail -5 $o/dbg$dbg.log; return 1; }
+    grep fit $o/dbg$dbg.log
+  done
+  timeout -k 10 600 python -u bench.py --workload c5 --no-cpu --alt-steps 0 --soak 0 > $o/c5.json 2> $o/c5.err || { tail -20 $o/c5.err; return 1; }
+  python -c "import json;l=json.load(open('$o/c5.json'));print('c5', l['value'], l['ms_per_step'], l['roofline']['frac'], l['roofline']['aggregation_frac'], l['check']['ok'], l['config']['groups'])"
+}
+
+r3s2h() {
+  o=gpurun_out/r3s2h; mkdir -p $o
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c5,--no-cpu,--alt-steps,0,--soak,0,--no-check --variant oma2= --variant oma1=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so --out $o/ab_c5.jsonl > $o/ab.log 2>&1 || { tail -20 $o/ab.log; return 1; }
+  tail -3 $o/ab.log
+}
+
+r3s2i() {
+  o=gpurun_out/r3s2i; mkdir -p $o
+  timeout -k 10 300 python -u tools/rb_probe.py > $o/cur.log 2>&1 || { tail -5 $o/cur.log; return 1; }
+  GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so timeout -k 10 300 python -u tools/rb_probe.py > $o/old.log 2>&1 || { tail -5 $o/old.log; return 1; }
+  echo cur; grep fit $o/cur.log; echo old; grep fit $o/old.log
+}
+
+r3s2j() {
+  o=gpurun_out/r3s2j; mkdir -p $o
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_resident_batched.py tests/test_gpu_c5_fullsize.py > $o/t.log 2>&1 || { tail -30 $o/t.log; return 1; }
+  tail -1 $o/t.log
+  timeout -k 10 300 python -u tools/rb_probe.py --quick > $o/probe_cur.log 2>&1 || { tail -5 $o/probe_cur.log; return 1; }
+  grep fit $o/probe_cur.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c5,--no-cpu,--alt-steps,0,--soak,0,--no-check --variant cur= --variant old=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so --out $o/ab_c5.jsonl > $o/ab.log 2>&1 || { tail -20 $o/ab.log; return 1; }
+  tail -2 $o/ab.log
+}
+
+r3s2l() {
+  o=gpurun_out/r3s2l; mkdir -p $o
+  timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_resident_batched.py tests/test_gpu_batched.py tests/test_gpu_c5_fullsize.py > $o/t.log 2>&1; rc=$?
+  tail -3 $o/t.log; grep -E "^FAILED|Error" $o/t.log | head
+  [ $rc -ne 0 ] && return $rc
+  timeout -k 10 900 python -u bench.py --workload c5 --no-cpu --soak 0 > $o/c5.json 2> $o/c5.err || { tail -20 $o/c5.err; return 1; }
+  python -c "import json;l=json.load(open('$o/c5.json'));print('c5', l['value'], json.dumps(l['alt_layout']))"
+}
+
+r3s2n() {
+  o=gpurun_out/r3s2n; mkdir -p $o
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c5,--no-cpu,--alt-steps,0,--soak,0,--no-check --variant perwave= --variant wave0=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so --out $o/ab_c5.jsonl > $o/ab.log 2>&1 || { tail -20 $o/ab.log; return 1; }
+  tail -2 $o/ab.log
+}
+
+r3s2o() {
+  o=gpurun_out/r3s2o; mkdir -p $o
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_weiszfeld.py tests/test_gpu_training.py tests/test_gpu_resident_batched.py > $o/t.log 2>&1 || { tail -30 $o/t.log; return 1; }
+  tail -1 $o/t.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant fast= --variant prev=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so --out $o/ab_c2.jsonl > $o/ab.log 2>&1 || { tail -20 $o/ab.log; return 1; }
+  tail -2 $o/ab.log
+}
+
+r3s2p() {
+  o=gpurun_out/r3s2p; mkdir -p $o
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_resident_batched.py > $o/t.log 2>&1 || { tail -30 $o/t.log; return 1; }
+  tail -1 $o/t.log
+  for dbg in 0 128 256 32; do
+    GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so GMAGG_RB_DBG=$dbg timeout -k 10 200 python -u tools/rb_probe.py --quick > $o/dbg$dbg.log 2>&1 || { tail -5 $o/dbg$dbg.log; return 1; }
+    grep fit $o/dbg$dbg.log
+  done
+  timeout -k 10 200 python -u tools/rb_probe.py --quick > $o/cur.log 2>&1 || { tail -5 $o/cur.log; return 1; }
+  grep fit $o/cur.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 2 --bench=--workload,c5,--no-cpu,--alt-steps,0,--soak,0,--no-check --variant cur= --variant prev=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so --out $o/ab_c5.jsonl > $o/ab.log 2>&1 || { tail -20 $o/ab.log; return 1; }
+  tail -2 $o/ab.log
+}
+
+r3s2q() {
+  o=gpurun_out/r3s2q; mkdir -p $o
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c5,--no-cpu,--alt-steps,0,--soak,0,--no-check --variant pf0= --variant pf10=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so --variant pf5=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt2.so --out $o/ab_c5.jsonl > $o/ab.log 2>&1 || { tail -20 $o/ab.log; return 1; }
+  tail -3 $o/ab.log
+  timeout -k 10 300 python -u tools/loop_bench.py > $o/loop.log 2>&1 || { tail -20 $o/loop.log; return 1; }
+  tail -8 $o/loop.log
+}
+
+r3s3_c2_layouts() {
+  # C2 (AirComp gm, K=50, d=7850, 1000 iterations): rows (C2 single resident kernel) vs panels
+  # (the batched resident kernel at P = 1), interleaved twice on one box
+  mkdir -p gpurun_out
+  for i in 1 2; do
+    timeout -k 10 120 python -u bench.py --workload c2 --steps 100 --warmup 5 --alt-steps 0 \
+      >> gpurun_out/r3s3_c2_rows.jsonl 2>> gpurun_out/r3s3_c2.err || return $?
+    timeout -k 10 120 python -u bench.py --workload c2 --layout panels --steps 100 --warmup 5 \
+      --alt-steps 0 >> gpurun_out/r3s3_c2_panels.jsonl 2>> gpurun_out/r3s3_c2.err || return $?
+  done
+}
+
+r3s3_c5air_pmc() {
+  # HBM traffic of the C5 AirComp reading's resident gm kernel: FETCH_SIZE and WRITE_SIZE,
+  # each in its own pass, then tools/pmc_summary.py
+  O=gpurun_out/c5air_pmc
+  mkdir -p $O
+  B="bench.py --workload c5 --reading aircomp --steps 1 --warmup 0 --no-cpu --alt-steps 0 --no-check"
+  timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/f -o p -- python3 $B > $O/f.json 2> $O/f.err &&
+  timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/w -o p -- python3 $B > $O/w.json 2> $O/w.err &&
+  python3 tools/pmc_summary.py $O/f/p_counter_collection.csv $O/w/p_counter_collection.csv $O/pmc.json "c5 aircomp reading, panels, resident" > $O/summary.txt 2>&1
+}
+
+r3s3_c5air_trace() {
+  # kernel trace of the C5 AirComp reading (gm, 1000 iterations per noisy problem) on the
+  # spill-free batched resident tile
+  mkdir -p gpurun_out/c5air
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5air/prof -o run -- \
+    python3 bench.py --workload c5 --reading aircomp --steps 1 --warmup 1 --no-cpu --alt-steps 0 \
+    > gpurun_out/c5air/bench.json 2> gpurun_out/c5air/bench.err
+}
+
+r3s3_panels1() {
+  # single-call panels -> batched resident kernel (P = 1): the panel / pre-noise tests, then the
+  # training loop bench on both layouts
+  mkdir -p gpurun_out
+  timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+    tests/test_gpu_panels.py tests/test_gpu_resident_batched.py \
+    "tests/test_gpu_weiszfeld.py::test_pre_oma_equals_oma_then_gm2" > gpurun_out/r3s3_panels1.log 2>&1 &&
+  timeout -k 10 200 python -u tools/loop_bench.py > gpurun_out/r3s3_loop.jsonl 2>&1
+}
+
+r3s3_rb_draws() {
+  # resident batched, AirComp draws drawn after the publish + r_k in LDS (no scratch at KR=50
+  # MODE 1) vs the previous library (libgmagg_alt.so: 352 B/lane of scratch): C2 on panels
+  # (P = 1), then C5 (gm2, must not move), C5's AirComp reading (gm, 1000 iterations); then the resident-batched GPU tests
+  mkdir -p gpurun_out
+  L=$PWD/byzantine_aircomp_amd/libgmagg_alt.so
+  timeout -k 10 300 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--layout,panels,--steps,100,--warmup,5,--alt-steps,0,--no-cpu \
+    --variant new= --variant old=GMAGG_LIB=$L --out gpurun_out/r3s3_rb_draws_c2_ab.jsonl > gpurun_out/r3s3_rb_draws_c2_ab.txt 2>&1 &&
+  timeout -k 10 300 python -u tools/ab.py --rounds 2 --bench=--workload,c5,--no-cpu,--alt-steps,0 \
+    --variant new= --variant old=GMAGG_LIB=$L --out gpurun_out/r3s3_rb_draws_c5_ab.jsonl > gpurun_out/r3s3_rb_draws_c5_ab.txt 2>&1 &&
+  timeout -k 10 400 python -u tools/ab.py --rounds 2 --bench=--workload,c5,--reading,aircomp,--steps,1,--warmup,1,--no-cpu,--alt-steps,0 \
+    --variant new= --variant old=GMAGG_LIB=$L --out gpurun_out/r3s3_rb_draws_c5air_ab.jsonl > gpurun_out/r3s3_rb_draws_c5air_ab.txt 2>&1 &&
+  timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+    tests/test_gpu_resident_batched.py tests/test_gpu_panels.py > gpurun_out/r3s3_rb_draws_tests.log 2>&1
+}
+
+r4s1e() {
+  O=gpurun_out/r4s1e; mkdir -p $O; export TMPDIR=/tmp
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_weiszfeld.py -q -x --timeout 200 --timeout-method thread -rf -p no:cacheprovider -k "c4_recipe or guard or gram_split" > $O/pytest.log 2>&1; tail -3 $O/pytest.log
+  GMAGG_GUARD_DEBUG=1 timeout -k 10 400 python -u bench.py --workload c4 --steps 5 --warmup 1 --no-cpu > $O/c4.json 2> $O/c4.err || { tail -5 $O/c4.err; return 3; }
+  grep "gram guard" $O/c4.err | tail -2; cut -c1-600 $O/c4.json
+  for dbg in 0 7; do GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so GMAGG_RB_DBG=$dbg timeout -k 10 200 python -u tools/rb_probe.py --quick > $O/rb_probe_dbg$dbg.log 2>&1 || return 4; tail -1 $O/rb_probe_dbg$dbg.log; done
+  GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so timeout -k 10 200 python -u bench.py --workload c2 --steps 10 --no-cpu --no-check --alt-steps 0 --soak 0 > $O/c2_exchange_only.json 2> $O/c2x.err || return 5
+  timeout -k 10 200 python -u bench.py --workload c2 --steps 10 --no-cpu --no-check --alt-steps 0 --soak 0 > $O/c2.json 2> $O/c2.err || return 6
+  python -c "
+  import json
+  for f in ('c2_exchange_only','c2'):
+      d=json.load(open('$O/'+f+'.json')); print(f, d['value'], d['roofline'].get('us_per_iteration'))"
+}
+
+r4s1f() {
+  # Round 4 session 1: latency-roofline probes (exchange floor, VALU instruction counts)
+  # and the whole-C4 Gram job's trace + PMC traffic.
+  O=gpurun_out/r4s1f; mkdir -p $O; export TMPDIR=/tmp
+  B="--no-cpu --no-check --alt-steps 0 --soak 0"
+  GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so timeout -k 10 200 python -u bench.py --workload c2 --tol -1 --steps 5 $B > $O/c2_exchange_only.json 2> $O/c2x.err || return 2
+  timeout -k 10 200 python -u bench.py --workload c2 --tol -1 --steps 5 $B > $O/c2_tolneg.json 2> $O/c2.err || return 3
+  for w in "c2:--workload c2 --steps 3" "c5air:--workload c5 --reading aircomp --steps 1 --warmup 0" "c5pre:--workload c5 --steps 1 --warmup 0"; do
+    n=${w%%:*}; a=${w#*:}
+    timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv -d $O/pmc_valu_$n -o p -- python3 bench.py $a $B > $O/pmc_valu_$n.log 2>&1 || return 4
+  done
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c4 -o t -- python3 bench.py --workload c4 --steps 3 --warmup 1 $B > $O/trace_c4.log 2>&1 || return 5
+  head -5 $O/trace_c4/t_kernel_stats.csv
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 400 rocprofv3 --pmc $c --output-format csv -d $O/pmc_c4_$c -o p -- python3 bench.py --workload c4 --steps 2 --warmup 1 $B > $O/pmc_c4_$c.log 2>&1 || return 6
+  done
+  ls -R $O | head -40
+}
+
+r4s1g() {
+  # Round 4 session 1: the closing check (GPU suite, smoke, default bench), then PMC of
+  # the f3 selection kernels (issue- or latency-bound?).
+  bash tools/final_check.sh || return $?
+  O=gpurun_out/r4s1g; mkdir -p $O; export TMPDIR=/tmp
+  timeout -k 10 120 python -u tools/select_bench.py --K 1000 --reps 3 > $O/select.log 2>&1 || return 5
+  cat $O/select.log
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY --output-format csv -d $O/pmc_sel -o p -- python3 tools/select_bench.py --K 1000 --reps 1 > $O/pmc_sel.log 2>&1 || return 6
+  timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_ACTIVE_INST_ANY --output-format csv -d $O/pmc_sel2 -o p -- python3 tools/select_bench.py --K 1000 --reps 1 > $O/pmc_sel2.log 2>&1 || return 7
+  echo pmc-done
+}
+
+[ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
+"$1"
