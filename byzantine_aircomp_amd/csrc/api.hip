@@ -97,6 +97,21 @@ unsigned checkin_need(unsigned blocks) {
   return blocks + ((e && atoi(e) != 0) ? 1u : 0u);
 }
 
+// XCD placement of the resident grids (read per call).  GMAGG_RES_XCD=1 (A/B, off): the
+// single-problem kernel's blocks all on one XCD when they fit its CUs (stride 8: only
+// blocks b % 8 == 0 work) — C2 172.8 vs 179.8 aggregations/s, kept off.  The batched
+// kernel's groups are numbered XCD by XCD (GMAGG_RB_XCD=0 turns it off): a group of 49
+// blocks spans 2-3 XCDs instead of 8, the AirComp exchange's traffic 259 -> 110 GB per
+// 1024-problem launch, the prenoise sweep 70.5k -> 71.6k problems/s.
+unsigned res_xcd_stride(int nb, int num_cu) {
+  const char* e = getenv("GMAGG_RES_XCD");
+  return (e && atoi(e) != 0 && nb <= num_cu / 8) ? 8u : 1u;
+}
+int rb_xcd_major() {
+  const char* e = getenv("GMAGG_RB_XCD");
+  return (e && atoi(e) == 0) ? 0 : 1;     // on by default (round 4 A/B)
+}
+
 // Stream-orders the context's workspace between calls (see gm_ctx::ws_ev): the
 // constructor makes `s` wait for the previous call's tail when that call ran on
 // another stream; the destructor marks the end of this call's work on `s`.
@@ -333,11 +348,12 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   a.gran = reinterpret_cast<unsigned long long*>(w.slab);
   a.checkin = a.gran + (size_t)2 * nb * S;      // (resident_gran_words: + nb + 1 slots)
   a.need = checkin_need((unsigned)nb);
+  a.stride = res_xcd_stride(nb, c->num_cu);
   a.bar = bar; a.st = w.st;
   hipEvent_t e0, e1;
   rc = record_pass_begin(c, s, &e0, &e1);
   if (rc) return rc;
-  HIPCHK(launch_resident(cfg, cpb, nb, a, s));
+  HIPCHK(launch_resident(cfg, cpb, nb * (int)a.stride, a, s));
   rc = record_pass_end(c, s, e0, e1);
   if (rc) return rc;
   KState* hst = reinterpret_cast<KState*>(c->host);
@@ -429,6 +445,7 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
   a.flag = flag;
   a.checkin = reinterpret_cast<unsigned long long*>(b + o_ci);
   a.need = checkin_need(nblocks);
+  a.xcd_major = rb_xcd_major();
   a.st = st;
   hipEvent_t e0, e1;
   rc = record_pass_begin(c, s, &e0, &e1);

@@ -383,6 +383,50 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
   }
 }
 
+// The order statistics of one column pair whose keys the wave holds (lane l: rows
+// l + 64 i): res[h] = the median (mode 0) or the trimmed mean (mode 1) of column h.
+// buf(h, q): LDS slots for chain (h, q)'s compaction, STR words apart.
+template <int R, int R2, int STR, typename Buf>
+__device__ __forceinline__ void select_pair(const uint32_t (&key)[2][R], const bool (&nan)[2],
+                                            int64_t K, int mode, int64_t b, Buf buf,
+                                            float (&res)[2]) {
+  if (mode == 0) {
+    const int64_t rk[1] = {(K - 1) / 2};
+    uint32_t ans[2][1];
+    select_ranks<R, 2, 1, R2, STR>(key, rk, ans, buf);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      res[h] = __ballot(nan[h]) ? __uint_as_float(0x7FC00000u) : key_value(ans[h][0]);
+  } else {
+    const int64_t rk[2] = {b, K - b - 1};
+    uint32_t ans[2][2];
+    select_ranks<R, 2, 2, R2, STR>(key, rk, ans, buf);
+    const int64_t n = K - 2 * b;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t lo = ans[h][0], hi = ans[h][1];
+      const float vlo = key_value(lo), vhi = key_value(hi);
+      double sum;
+      if (lo == hi) {
+        sum = (double)n * (double)vlo;
+      } else {
+        double sv = 0.0;
+        int64_t le_lo = 0, lt_hi = 0;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          if (key[h][i] > lo && key[h][i] < hi) sv += (double)key_value(key[h][i]);
+          le_lo += __popcll(__ballot(key[h][i] <= lo));
+          lt_hi += __popcll(__ballot(key[h][i] < hi));
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sv += __shfl_xor(sv, o);
+        sum = sv + (double)(le_lo - b) * (double)vlo + (double)((K - b) - lt_hi) * (double)vhi;
+      }
+      res[h] = (float)(sum / (double)n);
+    }
+  }
+}
+
 // The selection of one staged K x C tile (columns j0 .. j0 + C - 1).
 template <int R, int C, int NWV>
 __device__ __forceinline__ void select_tile(float (&tile)[64 * R][C + 1], int64_t K, int64_t d,
@@ -412,41 +456,7 @@ __device__ __forceinline__ void select_tile(float (&tile)[64 * R][C + 1], int64_
     auto buf = [&](int h, int q) {
       return reinterpret_cast<uint32_t*>(&tile[q * 64 * (R2 > 0 ? R2 : 1)][c0 + NWV * h]);
     };
-    if (mode == 0) {
-      const int64_t rk[1] = {(K - 1) / 2};
-      uint32_t ans[2][1];
-      select_ranks<R, 2, 1, R2, C + 1>(key, rk, ans, buf);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        res[h] = __ballot(nan[h]) ? __uint_as_float(0x7FC00000u) : key_value(ans[h][0]);
-    } else {
-      const int64_t rk[2] = {b, K - b - 1};
-      uint32_t ans[2][2];
-      select_ranks<R, 2, 2, R2, C + 1>(key, rk, ans, buf);
-      const int64_t n = K - 2 * b;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t lo = ans[h][0], hi = ans[h][1];
-        const float vlo = key_value(lo), vhi = key_value(hi);
-        double sum;
-        if (lo == hi) {
-          sum = (double)n * (double)vlo;
-        } else {
-          double sv = 0.0;
-          int64_t le_lo = 0, lt_hi = 0;
-#pragma unroll
-          for (int i = 0; i < R; ++i) {
-            if (key[h][i] > lo && key[h][i] < hi) sv += (double)key_value(key[h][i]);
-            le_lo += __popcll(__ballot(key[h][i] <= lo));
-            lt_hi += __popcll(__ballot(key[h][i] < hi));
-          }
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) sv += __shfl_xor(sv, o);
-          sum = sv + (double)(le_lo - b) * (double)vlo + (double)((K - b) - lt_hi) * (double)vhi;
-        }
-        res[h] = (float)(sum / (double)n);
-      }
-    }
+    select_pair<R, R2, C + 1>(key, nan, K, mode, b, buf, res);
     if (lane == 0) {
       out[j0 + c0] = res[0];
       if (j0 + c0 + NWV < d) out[j0 + c0 + NWV] = res[1];
@@ -742,6 +752,9 @@ hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, 
                          s, X, K, d, ldx, ws, mode, b, vec4, out);                              \
     }                                                                                           \
   } while (0)
+  // (round 4: gathering each wave's column pair straight from HBM, no LDS tile, so that
+  // VGPRs rather than two 69.6-KB tiles limit the CU: K=1000 x 2M median 21.0 vs 3.83 ms —
+  // 64 scattered 4-byte loads per wave instruction; profiles/r4s1_select_direct_ab.jsonl)
   // K <= 1024: 8 waves per 69.6-KB tile (one column pair each) so that the CU holds
   // 4 waves per SIMD (the LDS allows 2 tiles) instead of 2
   if (K <= 64) GMK_SEL(1, 32, 4);

@@ -238,7 +238,8 @@ __device__ __forceinline__ float xlane_wave_sum_f32(float v) {
 
 // Co-residency check-in of a plain-launched persistent grid (resident.hip,
 // resident_batched.hip), before a block reads or writes anything of the problem: block
-// b stores the tag into ci[b]; every block then waits, bounded by `ticks` of the 100 MHz
+// b stores the tag into ci[slot] (slot = its logical index); every block then waits,
+// bounded by `ticks` of the 100 MHz
 // real-time clock, until slots [0, need) all carry it (need = the grid's block count;
 // GMAGG_RES_CHECKIN_FAIL makes it one more, a slot nobody writes, to test the fallback).
 // A grid that is not co-resident (a shared GPU, CUs held by another stream's kernel)
@@ -250,7 +251,7 @@ __device__ __forceinline__ float xlane_wave_sum_f32(float v) {
 constexpr unsigned kCheckinTag = 0xC0DEC0DEu;
 constexpr uint64_t kCheckinTicks = 10000000ull;   // 100 ms
 
-__device__ __forceinline__ bool grid_checkin(unsigned long long* ci, unsigned need,
+__device__ __forceinline__ bool grid_checkin(unsigned long long* ci, unsigned slot, unsigned need,
                                              unsigned* tmo_word, unsigned* passed,
                                              uint64_t ticks, int* s_ok) {
   typedef __attribute__((address_space(1))) unsigned long long gu64_t;
@@ -260,7 +261,7 @@ __device__ __forceinline__ bool grid_checkin(unsigned long long* ci, unsigned ne
   const unsigned tid = threadIdx.x;
   if (tid == 0) {
     *s_ok = 1;
-    __hip_atomic_store(c + blockIdx.x, (unsigned long long)kCheckinTag << 32, __ATOMIC_RELAXED,
+    __hip_atomic_store(c + slot, (unsigned long long)kCheckinTag << 32, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();

@@ -119,6 +119,10 @@ struct ResArgs {
   unsigned* bar;         // [2] timeout flag, [3] check-in passed (zeroed per call)
   unsigned long long* checkin;   // [gridDim.x + 1] co-residency slots (zeroed per call)
   unsigned need;         // slots the check-in waits for (gridDim.x; + 1 forces a failure)
+  // 1, or 8: the grid is 8x the working blocks and only blocks b % 8 == 0 work (logical
+  // block b / 8), so that — workgroups being dispatched round-robin over the 8 XCDs — every
+  // working block sits on ONE XCD and the exchange stays inside its L2 (A/B knob)
+  unsigned stride;
   KState* st;
 };
 // Plan a resident launch over nch chunks: chunks per block and blocks (false: the
@@ -152,6 +156,10 @@ struct ResBArgs {
   unsigned* flag;         // [0] timeout flag, [2] check-in passed (zeroed per call)
   unsigned long long* checkin;   // [gridDim.x + 1] co-residency slots (zeroed per call)
   unsigned need;          // slots the check-in waits for (gridDim.x; + 1 forces a failure)
+  // 1: logical block = blockIdx.x (a group's NB blocks round-robin over all 8 XCDs);
+  // XCD-major: logical blocks numbered XCD by XCD (b % 8 first), so a group of NB blocks
+  // spans ceil(NB / 32) + 1 XCDs instead of 8 (A/B knob)
+  int xcd_major;
   KState* st;             // [P]
 };
 struct RbPlan {

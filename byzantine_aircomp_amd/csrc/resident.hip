@@ -176,15 +176,17 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   const int c = lane % LPR, q = lane / LPR;
   const int rg = w * QW + q;
   const int64_t K = a.K, d = a.d;
-  const unsigned nb = gridDim.x;
+  if (blockIdx.x % a.stride) return;                // (stride 8: a placeholder block)
+  const unsigned bid = blockIdx.x / a.stride;       // logical block
+  const unsigned nb = gridDim.x / a.stride;
   const int64_t NV = res_values<NW>(K);            // values per block and pass
-  const int64_t ch0 = (int64_t)blockIdx.x * CPB;   // first chunk of this block
+  const int64_t ch0 = (int64_t)bid * CPB;          // first chunk of this block
   const int64_t gj = ch0 * J + tid;                // finisher column (tid < JB)
   const bool fin = tid < JB && gj < d;
   gu64* gran = (gu64*)a.gran;                      // [2][nb][2 NV]
   gu32* tmo = (gu32*)a.bar + 2;
   // every block of the grid co-resident before anything is read (device_util.h)
-  if (!grid_checkin(a.checkin, a.need, a.bar + 2, a.bar + 3, kCheckinTicks, &s_ok)) return;
+  if (!grid_checkin(a.checkin, bid, a.need, a.bar + 2, a.bar + 3, kCheckinTicks, &s_ok)) return;
 
   // ---- the block's tiles: loaded once, resident for the whole call
   float x[CPB][R][V];
@@ -210,7 +212,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   };
   // publish this block's partials of pass p (granules, tag p + 1, buffer p & 1)
   auto publish = [&](int64_t p, const double* racc, const double* racc2, double mv, double gn) {
-    gu64* out = gran + ((p & 1) * nb + blockIdx.x) * NV;
+    gu64* out = gran + ((p & 1) * nb + bid) * NV;
     const unsigned tag = (unsigned)(p + 1);
     if ((c % SPAN) == 0) {
 #pragma unroll
@@ -530,14 +532,14 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
     RES_T(4)
   }
 #ifdef GMK_RES_PROF
-  if (blockIdx.x == 0 && threadIdx.x == 0)
+  if (bid == 0 && threadIdx.x == 0)
     printf("GMK_RES_PROF nb=%u CPB=%d iters=%ld ns/iter: gather %.0f coef %.0f phaseA %.0f "
            "phaseB %.0f publish %.0f\n", nb, CPB, (long)it, 10.0 * prof_[0] / it,
            10.0 * prof_[1] / it, 10.0 * prof_[2] / it, 10.0 * prof_[3] / it, 10.0 * prof_[4] / it);
 #endif
 
   if (fin) a.out[gj] = gcur;
-  if (blockIdx.x == 0 && tid == 0) {
+  if (bid == 0 && tid == 0) {
     a.st->iters = it;
     a.st->last_movement = last_mv;
     a.st->converged = conv;

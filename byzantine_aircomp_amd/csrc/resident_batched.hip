@@ -52,6 +52,10 @@ constexpr int kRbCols = 2048;                    // columns per block
 #endif
 
 constexpr uint64_t kRbPollTicks = 200000000ull;  // 2 s at the 100 MHz real-time clock
+// the poll's back-off between rounds, in units of 64 cycles (A/B knob)
+#ifndef GMK_RB_SLEEP
+#define GMK_RB_SLEEP 1
+#endif
 constexpr int kRbChunk = 8;                      // granules in flight per poll round
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -87,7 +91,7 @@ __device__ __forceinline__ bool rb_gather(const gu64* g, int64_t bstride, int fi
 #define GMK_RB_EARLY_H2 0
 #endif
 #ifndef GMK_RB_NOSLEEP
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(GMK_RB_SLEEP);
 #endif
       if (((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t0 > kRbPollTicks) ||
           __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -177,7 +181,15 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int NB = a.nb;
-  const int grp = (int)blockIdx.x / NB, bi = (int)blockIdx.x - grp * NB;
+  int lb = (int)blockIdx.x;                        // logical block
+  if (a.xcd_major) {
+    // XCD x = b % 8 holds blocks x, x + 8, ...: number them XCD by XCD
+    const int n = (int)gridDim.x, x = lb & 7;
+    int before = 0;
+    for (int y = 0; y < x; ++y) before += (n - y + 7) >> 3;
+    lb = before + (lb >> 3);
+  }
+  const int grp = lb / NB, bi = lb - grp * NB;
   const int NG = (int)gridDim.x / NB;
   const int64_t K = a.K, d = a.d;
   const int64_t NV = 2 * K + 2;                    // granule slots per block and pass
@@ -195,7 +207,8 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   if (tid < NW * KC) (&s_coef[0][0])[tid] = 0.f;
   // every block of the grid co-resident before any problem's X is read or (pre-noise)
   // written: a grid that is not fails here with X untouched (device_util.h)
-  if (!grid_checkin(a.checkin, a.need, a.flag, a.flag + 2, kCheckinTicks, &s_ok)) return;
+  if (!grid_checkin(a.checkin, blockIdx.x, a.need, a.flag, a.flag + 2, kCheckinTicks, &s_ok))
+    return;
 
   f4 x[KV > 0 ? KV : 1];   // the tile's register rows: row k of the thread's 4 columns
   float g[4];              // the iterate at those columns

@@ -224,5 +224,64 @@ r4s1g() {
   echo pmc-done
 }
 
+r4s1h() {
+  # f3 selection: the LDS-tile kernel vs the direct-gather kernel (GMAGG_SELECT_DIRECT=1),
+  # interleaved, plus the f3 parity tests on the direct kernel
+  O=gpurun_out/r4s1h; mkdir -p $O
+  GMAGG_SELECT_DIRECT=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_other_aggregators.py > $O/t_direct.log 2>&1 || { tail -30 $O/t_direct.log; return 1; }
+  tail -1 $O/t_direct.log
+  for r in 1 2; do
+    for v in 0 1; do
+      GMAGG_SELECT_DIRECT=$v timeout -k 10 120 python -u tools/select_bench.py --K 1000 256 --reps 3 >> $O/select_direct$v.jsonl 2> $O/sel.err || return 2
+    done
+  done
+  cat $O/select_direct*.jsonl
+}
+
+r4s1i() {
+  # XCD placement of the resident grids: C2's 31 blocks on one XCD (GMAGG_RES_XCD=1),
+  # the C5 groups numbered XCD by XCD (GMAGG_RB_XCD=1); parity first, then A/B
+  O=gpurun_out/r4s1i; mkdir -p $O
+  GMAGG_RES_XCD=1 GMAGG_RB_XCD=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_resident_batched.py tests/test_gpu_weiszfeld.py -k "resident or gm_host or philox or gm2_matches or clamp" > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  timeout -k 10 600 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant base= --variant xcd=GMAGG_RES_XCD=1 --out $O/ab_c2.jsonl > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; return 2; }
+  tail -3 $O/ab_c2.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 2 --bench=--workload,c5,--reading,aircomp,--no-cpu,--alt-steps,0,--soak,0,--no-check,--steps,1,--warmup,0 --variant base= --variant xcd=GMAGG_RB_XCD=1 --out $O/ab_c5air.jsonl > $O/ab_c5air.log 2>&1 || { tail -20 $O/ab_c5air.log; return 3; }
+  tail -3 $O/ab_c5air.log
+  timeout -k 10 600 python -u tools/ab.py --rounds 3 --bench=--workload,c5,--no-cpu,--alt-steps,0,--soak,0,--no-check --variant base= --variant xcd=GMAGG_RB_XCD=1 --out $O/ab_c5.jsonl > $O/ab_c5.log 2>&1 || { tail -20 $O/ab_c5.log; return 4; }
+  tail -3 $O/ab_c5.log
+}
+
+r4s1j() {
+  # HBM traffic (FETCH_SIZE / WRITE_SIZE, one counter per pass) of the C5 AirComp reading's
+  # resident gm kernel, groups round-robin over the XCDs (base) vs numbered XCD by XCD
+  O=gpurun_out/r4s1j; mkdir -p $O
+  B="bench.py --workload c5 --reading aircomp --steps 1 --warmup 0 --no-cpu --alt-steps 0 --no-check --soak 0"
+  for v in 0 1; do
+    for c in FETCH_SIZE WRITE_SIZE; do
+      GMAGG_RB_XCD=$v timeout -s KILL 200 rocprofv3 --pmc $c --output-format csv -d $O/x$v_$c -o p -- python3 $B > $O/x${v}_$c.log 2>&1 || return 1
+      mv $O/x$v_$c $O/x${v}_$c
+    done
+    python3 tools/pmc_summary.py $O/x${v}_FETCH_SIZE/p_counter_collection.csv $O/x${v}_WRITE_SIZE/p_counter_collection.csv $O/pmc_x$v.json "c5 aircomp, GMAGG_RB_XCD=$v" > $O/summary_x$v.txt 2>&1 || return 2
+    grep resident $O/summary_x$v.txt
+  done
+}
+
+r4s1k() {
+  # the batched resident kernel's poll back-off: s_sleep 1 (product) vs 4 (libgmagg_alt.so,
+  # make alt ALT_FLAGS=-DGMK_RB_SLEEP=4): C5 AirComp throughput and exchange traffic
+  O=gpurun_out/r4s1k; mkdir -p $O
+  timeout -k 10 900 python -u tools/ab.py --rounds 2 --bench=--workload,c5,--reading,aircomp,--no-cpu,--alt-steps,0,--soak,0,--no-check,--steps,1,--warmup,0 --variant s1= --variant s4=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so --out $O/ab_c5air.jsonl > $O/ab_c5air.log 2>&1 || { tail -20 $O/ab_c5air.log; return 1; }
+  tail -2 $O/ab_c5air.log
+  timeout -k 10 600 python -u tools/ab.py --rounds 2 --bench=--workload,c5,--no-cpu,--alt-steps,0,--soak,0,--no-check --variant s1= --variant s4=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so --out $O/ab_c5.jsonl > $O/ab_c5.log 2>&1 || { tail -20 $O/ab_c5.log; return 2; }
+  tail -2 $O/ab_c5.log
+  B="bench.py --workload c5 --reading aircomp --steps 1 --warmup 0 --no-cpu --alt-steps 0 --no-check --soak 0"
+  for c in FETCH_SIZE WRITE_SIZE; do
+    GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so timeout -s KILL 200 rocprofv3 --pmc $c --output-format csv -d $O/s4_$c -o p -- python3 $B > $O/s4_$c.log 2>&1 || return 3
+  done
+  python3 tools/pmc_summary.py $O/s4_FETCH_SIZE/p_counter_collection.csv $O/s4_WRITE_SIZE/p_counter_collection.csv $O/pmc_s4.json "c5 aircomp, sleep 4" > $O/summary_s4.txt 2>&1 || return 4
+  grep resident $O/summary_s4.txt
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
