@@ -146,6 +146,8 @@ def pmc_traffic(workload, layout, kernel="weiszfeld_pass", mode="0"):
     import re
     files = [f for f in glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}_*.json"))]
     files += glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}.json"))
+    if "aircomp" not in workload:    # (r3s3_pmc_c5_aircomp_*: the other C5 reading's pass)
+        files = [f for f in files if "aircomp" not in os.path.basename(f)]
     for path in sorted(files, key=profile_order, reverse=True):
         data = json.load(open(path))
         for name, row in data["kernels"].items():
@@ -438,12 +440,13 @@ def run_c5(args, json_out, rank=0, world=1):
         hbm_bytes = sum(((2 if (args.reading == "prenoise" and var > 0) else 1)
                          * g0.shape[0] * 4.0 * K * d) for _, var, _, _, g0, _ in groups)
         per_launch = hbm_bytes / max(launches / max(args.steps, 1), 1)
-        # (the PMC on record is a pass over the prenoise reading's launches: quoted for
-        # that reading only, never beside another reading's algorithmic bytes)
+        # (each reading quotes the PMC pass of its own launches: the prenoise reading's
+        # gm2 kernel, the aircomp reading's gm kernel — the launch that dominates the sweep)
         traffic, traffic_src = (pmc_traffic("c5", "panels" if use_panels else "rows",
-                                            kernel="weiszfeld_resident_batched")
+                                            kernel="weiszfeld_resident_batched<50, 32, 0")
                                 if args.reading == "prenoise" else
-                                (None, "no PMC pass on record for the aircomp reading"))
+                                pmc_traffic("c5-aircomp", "panels" if use_panels else "rows",
+                                            kernel="weiszfeld_resident_batched<50, 32, 1"))
         achieved = hbm_bytes * args.steps / (pass_ms / 1e3) / 1e9 if pass_ms > 0 else None
         # The kernel is latency-bound: each iteration is a cross-CU exchange of every block's
         # partials plus the phases' VALU work, with the problem's tile on chip.  Roofline =

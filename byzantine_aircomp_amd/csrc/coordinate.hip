@@ -464,6 +464,10 @@ __device__ __forceinline__ void select_tile(float (&tile)[64 * R][C + 1], int64_
   }
 }
 
+#ifndef GMK_SELECT_DBG
+#define GMK_SELECT_DBG 0
+#endif
+
 // PERSIST: one grid of co-resident blocks walks the tiles (grid stride), each block
 // loading tile t + grid into registers while its waves select tile t's columns, so the
 // loads of a CU are in flight during its selection instead of only between tiles (the
@@ -515,14 +519,22 @@ __global__ void __launch_bounds__(NWV * 64) col_select(const float* __restrict__
   };
   int64_t v = blockIdx.x;
   if (v >= ntiles) return;
-  load(tile_of(v));
+  // GMK_SELECT_DBG (probe builds; 0 in the product): 1 = load + stage the tile only (no
+  // selection), 2 = every block loads one of 64 tiles (L2 / Infinity-Cache resident) and
+  // selects it: the two phases priced apart
+  auto src_tile = [&](int64_t u) { return GMK_SELECT_DBG == 2 ? tile_of(u % 64) : tile_of(u); };
+  load(src_tile(v));
   for (; v < ntiles; v += PERSIST ? (int64_t)gridDim.x : ntiles) {
     const int64_t j0 = tile_of(v) * C;
     if (PERSIST) __syncthreads();          // the previous tile's columns are in registers
     store();
     __syncthreads();
-    if (PERSIST && v + gridDim.x < ntiles) load(tile_of(v + gridDim.x));
-    select_tile<R, C, NWV>(tile, K, d, j0, mode, b, out);
+    if (PERSIST && v + gridDim.x < ntiles) load(src_tile(v + gridDim.x));
+    if constexpr (GMK_SELECT_DBG == 1) {
+      if (threadIdx.x < C && j0 + threadIdx.x < d) out[j0 + threadIdx.x] = tile[threadIdx.x][threadIdx.x];
+    } else {
+      select_tile<R, C, NWV>(tile, K, d, j0, mode, b, out);
+    }
   }
 }
 // Krum, step 1: squared distances of every row pair, register-tiled.

@@ -283,5 +283,18 @@ r4s1k() {
   grep resident $O/summary_s4.txt
 }
 
+r4s1l() {
+  # the f3 selection's phases priced apart (K=1000 x 2M): product vs load-and-stage only
+  # (libgmagg_sel1.so: -DGMK_SELECT_DBG=1) vs select on L2-resident tiles (sel2: DBG=2)
+  O=gpurun_out/r4s1l; mkdir -p $O
+  for r in 1 2; do
+    for v in prod sel1 sel2; do
+      lib=byzantine_aircomp_amd/libgmagg.so; [ $v != prod ] && lib=byzantine_aircomp_amd/libgmagg_$v.so
+      GMAGG_LIB=$lib timeout -k 10 120 python -u tools/select_bench.py --K 1000 --reps 3 2> $O/err.log | sed "s/}$/, \"lib\": \"$v\"}/" >> $O/phases.jsonl || return 1
+    done
+  done
+  cat $O/phases.jsonl
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
