@@ -223,6 +223,25 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 
+// Inclusive prefix sum over the wave of a per-lane int (the DPP sequence of wave_sum_i32
+// without its final read of lane 63).
+__device__ __forceinline__ int wave_scan_i32(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+  return v;
+}
+
+// GMK_SELECT_HIST=1 (A/B): the top byte of every chain's answer from ONE histogram of the
+// keys' top bytes (256 bins in LDS, one atomic add per held key, a wave prefix scan), shared
+// by a column's ranks, instead of 8 counting steps over every key.
+#ifndef GMK_SELECT_HIST
+#define GMK_SELECT_HIST 0
+#endif
+
 // Candidate compaction (round 2).  Before step `bit` a chain's answer lies in
 // [L, L + 2^(bit+1)); the step's count n = #(key < L + 2^bit) is also the count
 // below one end of the new interval, so the number of keys still in it (chi - clo)
@@ -369,7 +388,70 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
           }
       }
     };
-    select_steps<NC, NR>(31, 24, ans, clo, chi, rr, full);
+    if constexpr (GMK_SELECT_HIST) {
+      // bins of column c: buf(c, 0)[b * STR], b < 256 (the wave's own dead tile column)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        uint32_t* h = buf(c, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) h[(4 * lane + j) * STR] = 0u;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        uint32_t* h = buf(c, 0);
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+          __hip_atomic_fetch_add(&h[(key[c][i] >> 24) * STR], 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WAVEFRONT);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const uint32_t* h = buf(c, 0);
+        int hb[4], sl = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          hb[j] = (int)h[(4 * lane + j) * STR];
+          sl += hb[j];
+        }
+        const int incl = wave_scan_i32(sl), excl = incl - sl;
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+          // the lane whose 4 bins hold rank rr[q] (the bins count all 64 R keys, padding
+          // included, and rr < K <= 64 R: exactly one lane)
+          const uint64_t m = __ballot(excl <= rr[q] && rr[q] < incl);
+          const int L = __builtin_amdgcn_readfirstlane(__builtin_ctzll(m));
+          int lo = __builtin_amdgcn_readlane(excl, L);
+          int bsel = 4 * L + 3, blo = lo, bhi = 64 * R;
+          bool found = false;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int hj = __builtin_amdgcn_readlane(hb[j], L);
+            if (!found && lo + hj > rr[q]) {
+              found = true;
+              bsel = 4 * L + j;
+              blo = lo;
+              bhi = lo + hj;
+            }
+            lo += hj;
+          }
+          ans[c][q] = (uint32_t)bsel << 24;     // keys < ans: blo; keys < ans + 2^24: bhi
+          clo[c][q] = blo;
+          chi[c][q] = bhi;
+        }
+      }
+      // (the compaction below reuses the same LDS slots: the bins are consumed)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+      select_steps<NC, NR>(31, 24, ans, clo, chi, rr, full);
+    }
     if (small()) {
       finish_compacted(24);
       return;

@@ -602,6 +602,11 @@ def test_pre_oma_strided_view_is_noised_in_place():
     gm2_batched(vb, {"maxiter": 30, "tol": 1e-5, "guess": gb, "pre_oma_var": 1e-2,
                      "pre_oma_seed": 9})
     assert torch.equal(vb, vref)
+    # the default guess (the mean of the NOISY rows): the separate OMA runs first, on the
+    # packed copy, and must land in the caller's view as well
+    vc = bb[:, :, :d].transpose(0, 1).contiguous().transpose(0, 1)
+    gm2_batched(vc, {"maxiter": 30, "tol": 1e-5, "pre_oma_var": 1e-2, "pre_oma_seed": 9})
+    assert torch.equal(vc, vref)
 
 
 def test_pre_oma_host_draws_keep_reference_sequence():
