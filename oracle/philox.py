@@ -74,6 +74,33 @@ def oma_philox(X: np.ndarray, noise_var: float, seed: int, col_off: int = 0) -> 
 STREAM_FILL = 0x46494C4C
 
 
+_FILL_LIB = None
+
+
+def _fill_lib():
+    """oracle/_philox_fill.so (oracle/philox_fill.c, built by __graft_entry__.build() or on
+    first use with gcc), or None: the numpy restatement below is then used."""
+    global _FILL_LIB
+    if _FILL_LIB is None:
+        import ctypes
+        import os
+        import subprocess
+        here = os.path.dirname(os.path.abspath(__file__))
+        so, src = os.path.join(here, "_philox_fill.so"), os.path.join(here, "philox_fill.c")
+        try:
+            if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+                subprocess.run(["gcc", "-O2", "-fopenmp", "-shared", "-fPIC", src, "-o", so, "-lm"],
+                               check=True, capture_output=True)
+            lib = ctypes.CDLL(so)
+            i64, u64, f64, fp = ctypes.c_int64, ctypes.c_uint64, ctypes.c_double, ctypes.c_void_p
+            lib.fill_clients.argtypes = [i64, i64, i64, f64, f64, f64, f64, u64, i64, fp]
+            lib.fill_normal.argtypes = [i64, f64, f64, u64, i64, fp]
+            _FILL_LIB = lib
+        except (OSError, subprocess.CalledProcessError):
+            _FILL_LIB = False
+    return _FILL_LIB or None
+
+
 def fill_clients(K: int, d: int, B: int, mu_h: float, sd_h: float, mu_b: float, sd_b: float,
                  seed: int, col_off: int = 0) -> np.ndarray:
     """The synthetic client matrix of ``gm_fill_clients_f32`` (oma.hip fill_clients):
@@ -81,6 +108,11 @@ def fill_clients(K: int, d: int, B: int, mu_h: float, sd_h: float, mu_b: float, 
     c >> 2) on the fill stream; the last B rows take (mu_b, sd_b).  float32 of the
     float64 Box-Muller: the device's fast sin/cos put it within ~1e-6 of this, enough
     to decide whether a test input is well posed (tests/test_iteration_wellposed.py)."""
+    lib = _fill_lib()
+    if lib is not None:
+        X = np.empty((K, d), dtype=np.float32)
+        lib.fill_clients(K, d, B, mu_h, sd_h, mu_b, sd_b, seed, col_off, X.ctypes.data)
+        return X
     cols = col_off + np.arange(d, dtype=np.uint64)
     X = np.empty((K, d), dtype=np.float32)
     for k in range(K):
@@ -94,6 +126,11 @@ def fill_clients(K: int, d: int, B: int, mu_h: float, sd_h: float, mu_b: float, 
 def fill_normal(n: int, mu: float, sd: float, seed: int, off: int = 0) -> np.ndarray:
     """``gm_fill_normal_f32`` (oma.hip fill_normal): normal c & 3 of block
     (iteration 0xFFFFFFFF, index c >> 2)."""
+    lib = _fill_lib()
+    if lib is not None:
+        v = np.empty(n, dtype=np.float32)
+        lib.fill_normal(n, mu, sd, seed, off, v.ctypes.data)
+        return v
     cols = off + np.arange(n, dtype=np.uint64)
     z = normal4(seed, STREAM_FILL, np.uint64(0xFFFFFFFF), cols >> np.uint64(2))
     v = np.take_along_axis(z, (cols & np.uint64(3)).astype(np.int64)[:, None], axis=1)[:, 0]

@@ -196,10 +196,12 @@ def test_sharded_pre_oma_world1(world1, layout):
 
 
 def iteration_cases():
-    """(tests/test_iteration_wellposed.py) The +-1 inputs above are the device-filled C3 /
-    C4 recipes at 1000 x 200k and 256 x 2^19: too large for the CPU restatement of the
-    fill within the CPU suite.  Their ||g|| (the GM of N(0, 0.05^2) rows: ~0.0018 sqrt(d)
-    = 0.8 at K = 1000, ~0.0066 sqrt(d) = 4.8 at K = 256) puts the fp32 movement floor
-    (4 * 2^-24 ||g||) at 2e-7 / 1.1e-6, well under tol = 1e-5; the same recipe at
-    1000 x 65,536 is checked through test_gpu_fullsize.iteration_cases."""
-    return []
+    """The +-1 inputs above (the device fill restated by oracle/philox_fill.c) for
+    tests/test_iteration_wellposed.py."""
+    from oracle.philox import fill_clients, fill_normal
+
+    def fill(K, d, B, seed=20211):
+        return (torch.from_numpy(fill_clients(K, d, B, 0.0, 0.05, 0.25, 0.5, seed)),
+                torch.from_numpy(fill_normal(d, 0.0, 0.01, seed + 1)))
+    return [("gm2_world1_1000x200k", lambda: [(*fill(1000, 200_000, 200), 1000, 1e-5)]),
+            ("gram_world1_256x2^19", lambda: [(*fill(256, 1 << 19, 51), 1000, 1e-5)])]

@@ -168,4 +168,12 @@ def iteration_cases():
         X = torch.from_numpy(fill_clients(K, d, 200, 0.0, 0.05, 0.25, 0.5, 20211))
         g0 = torch.from_numpy(fill_normal(d, 0.0, 0.01, 20212))
         return [(X, g0, 1000, 1e-5)]
-    return [("c3_tile", c3_tile)]
+
+    def workspace_streams():           # test_workspace_ordered_across_streams' two inputs
+        out = []
+        for seed in (5, 6):
+            X = torch.from_numpy(fill_clients(1000, 1 << 16, 200, 0.0, 0.05, 0.25, 0.5, seed))
+            out.append((X, torch.from_numpy(fill_normal(1 << 16, 0.0, 0.01, seed + 1)), 1000,
+                        1e-5))
+        return out
+    return [("c3_tile", c3_tile), ("workspace_streams", workspace_streams)]

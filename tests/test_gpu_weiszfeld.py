@@ -634,11 +634,10 @@ def test_pre_oma_host_draws_keep_reference_sequence():
 
 
 def iteration_cases():
-    """The +-1 inputs above, on the CPU (tests/test_iteration_wellposed.py).  Not here:
-    the Gram-vs-streaming equalities at K = 256 x d = 1M / 4M on the device-filled C4
-    recipe (test_gram_matches_stream_at_c4_scale, test_gram_split_vs_f32_and_auto_choice,
-    test_gram_f16_split_matches_bf16_split): the CPU restatement of the fill is too slow
-    for the CPU suite at that size; their ||g|| (6.6 / 13) puts delta at 1.6e-6 / 3.1e-6."""
+    """The +-1 inputs above, on the CPU (tests/test_iteration_wellposed.py); the
+    device-filled C4-recipe inputs through oracle/philox_fill.c.  Not here: the
+    Gram-vs-streaming equality at K = 256 x d = 4M (test_gram_matches_stream_at_c4_scale):
+    16 GB of fp64 for the exact iteration; its ||g|| ~ 13 puts delta at 3.1e-6."""
     from conftest import golden_case, golden_names
     cases = []
     for name in golden_names("gm2"):
@@ -671,4 +670,17 @@ def iteration_cases():
             return [(X, p, 30, 1e-5, "windowed")]
         cases.append((f"guard_{case}", t))
     cases.append(("spike", lambda: [(*_spike_data(1e6), 1000, 1e-5)]))
+    from oracle.philox import fill_clients, fill_normal
+
+    def c4_like(K, d, seed=20211, shift=0.0, flag=()):
+        X = torch.from_numpy(fill_clients(K, d, K // 5, 0.0, 0.05, 0.25, 0.5, seed)) + shift
+        g0 = torch.from_numpy(fill_normal(d, 0.0, 0.01, seed + 1)) + shift
+        return [(X, g0, 1000, 1e-5, *flag)]
+    # (_c4_like on the device: gram_split_vs_f32 seed 20211, f16_vs_bf16 seed 777, the C4
+    # recipe vs the oracle seed 4040, shifted by 0.07 into the floor band: windowed)
+    cases.append(("c4like_256x2^20_s20211", lambda: c4_like(256, 1 << 20)))
+    cases.append(("c4like_256x2^20_s777", lambda: c4_like(256, 1 << 20, seed=777)))
+    cases.append(("c4like_256x2^20_s4040", lambda: c4_like(256, 1 << 20, seed=4040)))
+    cases.append(("c4like_256x2^20_s4040_shift", lambda: c4_like(256, 1 << 20, seed=4040,
+                                                                 shift=0.07, flag=("windowed",))))
     return cases

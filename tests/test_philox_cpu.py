@@ -25,3 +25,22 @@ def test_normal4_vectorised_and_moments():
     one = normal4(1234, 0x4F4D414E, np.uint64(0), np.uint64(777))
     assert np.array_equal(one, z[777])
     assert abs(z.mean()) < 0.01 and abs(z.var() - 1.0) < 0.01
+
+
+def test_fill_c_restatement_matches_numpy():
+    """oracle/philox_fill.c (the fast restatement of the device fill used for large
+    well-posedness inputs) agrees bit for bit with the numpy restatement."""
+    import numpy as np
+
+    import oracle.philox as ph
+    lib = ph._fill_lib()
+    assert lib is not None, "gcc could not build oracle/_philox_fill.so"
+    a = ph.fill_clients(9, 1003, 3, 0.0, 0.05, 0.25, 0.5, 777, col_off=5)
+    b = ph.fill_normal(1003, 0.0, 0.01, 99, off=7)
+    saved, ph._FILL_LIB = ph._FILL_LIB, False
+    try:
+        a2 = ph.fill_clients(9, 1003, 3, 0.0, 0.05, 0.25, 0.5, 777, col_off=5)
+        b2 = ph.fill_normal(1003, 0.0, 0.01, 99, off=7)
+    finally:
+        ph._FILL_LIB = saved
+    assert np.array_equal(a, a2) and np.array_equal(b, b2)
