@@ -311,5 +311,19 @@ r4s1m() {
   cat $O/ab.jsonl
 }
 
+r4s1n() {
+  # multi-rank rehearsals on one GPU after the round-4 changes: bench.py's N > 1 path
+  # (torchrun, gloo, the torch all-reduce callback) for C3-small and for the whole C4 job
+  # (d sharded in 2; the Gram guard decided on the all-reduced ||g||), then rank 0's
+  # shard of an 8-GPU C4 job (its per-rank time before the cross-GPU all-reduce latency)
+  O=gpurun_out/r4s1n; mkdir -p $O
+  for w in c3-small c4; do
+    timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --one-gpu --workload $w --no-cpu --alt-steps 0 --soak 0 --steps 3 --warmup 1 > $O/n2_$w.json 2> $O/n2_$w.err || { tail -20 $O/n2_$w.err; return 1; }
+    cut -c1-900 $O/n2_$w.json
+  done
+  timeout -k 10 400 python -u bench.py --dist --rehearse-shard 8 --workload c4 --no-cpu --alt-steps 0 --soak 0 --steps 10 --warmup 2 > $O/c4_shard8.json 2> $O/c4_shard8.err || { tail -20 $O/c4_shard8.err; return 2; }
+  cut -c1-900 $O/c4_shard8.json
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
