@@ -237,7 +237,9 @@ __device__ __forceinline__ int wave_scan_i32(int v) {
 
 // GMK_SELECT_HIST=1 (A/B): the top byte of every chain's answer from ONE histogram of the
 // keys' top bytes (256 bins in LDS, one atomic add per held key, a wave prefix scan), shared
-// by a column's ranks, instead of 8 counting steps over every key.
+// by a column's ranks, instead of 8 counting steps over every key; =2 also the next byte
+// (a histogram of the keys inside the chain's top-byte bin) when the top byte left more
+// candidates than the compaction takes.
 #ifndef GMK_SELECT_HIST
 #define GMK_SELECT_HIST 0
 #endif
@@ -456,7 +458,75 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
       finish_compacted(24);
       return;
     }
-    select_steps<NC, NR>(23, 16, ans, clo, chi, rr, full);
+    if constexpr (GMK_SELECT_HIST >= 2 && R >= 8) {
+      // bits 23..16 from a second histogram per chain: the keys inside the chain's top-byte
+      // bin, binned by their next byte (slots 256 q + b of column c's dead tile column)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        uint32_t* h = buf(c, 0);
+#pragma unroll
+        for (int q = 0; q < NR; ++q)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) h[(256 * q + 4 * lane + j) * STR] = 0u;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        uint32_t* h = buf(c, 0);
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+          const uint32_t top = ans[c][q] >> 24;
+#pragma unroll
+          for (int i = 0; i < R; ++i)
+            if ((key[c][i] >> 24) == top)
+              __hip_atomic_fetch_add(&h[(256 * q + ((key[c][i] >> 16) & 255u)) * STR], 1u,
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const uint32_t* h = buf(c, 0);
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+          int hb[4], sl = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            hb[j] = (int)h[(256 * q + 4 * lane + j) * STR];
+            sl += hb[j];
+          }
+          const int incl = wave_scan_i32(sl) + clo[c][q], excl = incl - sl;
+          const uint64_t m = __ballot(excl <= rr[q] && rr[q] < incl);
+          const int L = __builtin_amdgcn_readfirstlane(__builtin_ctzll(m));
+          int lo = __builtin_amdgcn_readlane(excl, L);
+          int bsel = 4 * L + 3, blo = lo, bhi = chi[c][q];
+          bool found = false;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int hj = __builtin_amdgcn_readlane(hb[j], L);
+            if (!found && lo + hj > rr[q]) {
+              found = true;
+              bsel = 4 * L + j;
+              blo = lo;
+              bhi = lo + hj;
+            }
+            lo += hj;
+          }
+          ans[c][q] |= (uint32_t)bsel << 16;
+          clo[c][q] = blo;
+          chi[c][q] = bhi;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+      select_steps<NC, NR>(23, 16, ans, clo, chi, rr, full);
+    }
     if (small()) {
       finish_compacted(16);
       return;

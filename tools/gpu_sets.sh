@@ -297,13 +297,16 @@ r4s1l() {
 }
 
 r4s1m() {
-  # the f3 selection's top byte from one LDS histogram (libgmagg_hist.so: -DGMK_SELECT_HIST=1)
-  # vs 8 counting steps (product): parity of the f3 tests on it, then interleaved timing
+  # the f3 selection's top byte (libgmagg_hist.so: -DGMK_SELECT_HIST=1) and top two bytes
+  # (hist2: =2) from LDS histograms vs counting steps (product): parity of the f3 tests on
+  # each, then interleaved timing
   O=gpurun_out/r4s1m; mkdir -p $O
-  GMAGG_LIB=byzantine_aircomp_amd/libgmagg_hist.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_other_aggregators.py tests/test_gpu_training.py -k "median or trimmed or select or other" > $O/t_hist.log 2>&1 || { tail -30 $O/t_hist.log; return 1; }
-  tail -1 $O/t_hist.log
+  for v in hist hist2; do
+    GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_other_aggregators.py > $O/t_$v.log 2>&1 || { tail -30 $O/t_$v.log; return 1; }
+    tail -1 $O/t_$v.log
+  done
   for r in 1 2; do
-    for v in prod hist; do
+    for v in prod hist hist2; do
       lib=byzantine_aircomp_amd/libgmagg.so; [ $v != prod ] && lib=byzantine_aircomp_amd/libgmagg_$v.so
       GMAGG_LIB=$lib timeout -k 10 120 python -u tools/select_bench.py --K 1000 256 --reps 3 2> $O/err.log | sed "s/}$/, \"lib\": \"$v\"}/" >> $O/ab.jsonl || return 2
     done
