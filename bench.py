@@ -889,8 +889,9 @@ def main():
             # block's partials plus the phases' VALU work.  Roofline: time per iteration
             # against the exchange floor (the kernel with its compute phases skipped, profiles/)
             us_it = avg_pass_s * 1e6 / max(res.iters, 1)
-            fl, fl_src = latency_floor("weiszfeld_resident" if layout == "rows"
-                                       else "weiszfeld_resident_batched")
+            # (the floor on record is C2's own shape on rows; a panels call runs the batched
+            # kernel with P = 1, whose floor was measured at C5's shape only: not quoted)
+            fl, fl_src = latency_floor("weiszfeld_resident") if layout == "rows" else (None, None)
             floor = fl["exchange_floor_us_per_iteration"] if fl else None
             roof = {"bound": "latency", "unit": "us per iteration", "achieved": us_it,
                     "peak": floor, "frac": floor / us_it if floor else None,
