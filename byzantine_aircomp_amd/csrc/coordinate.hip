@@ -235,13 +235,20 @@ __device__ __forceinline__ int wave_scan_i32(int v) {
   return v;
 }
 
-// GMK_SELECT_HIST=1 (A/B): the top byte of every chain's answer from ONE histogram of the
-// keys' top bytes (256 bins in LDS, one atomic add per held key, a wave prefix scan), shared
-// by a column's ranks, instead of 8 counting steps over every key; =2 also the next byte
-// (a histogram of the keys inside the chain's top-byte bin) when the top byte left more
-// candidates than the compaction takes.
+// The trimmed mean's two ranks (round 4): the top byte of each chain's answer from ONE
+// histogram of the keys' top bytes (256 bins in LDS, one atomic add per held key, a wave
+// prefix scan), shared by the column's two ranks, instead of 8 counting steps per rank over
+// every key; then, when the top byte left more candidates than the compaction takes, the
+// next byte from a histogram of the keys inside each rank's top-byte bin.  K=1000 x 2M:
+// 7.26 -> 6.30 ms; the median (one rank) measured slower with it, 3.81 -> 4.23 ms (the
+// adds to the few bins a column's top bytes fill serialize), so it keeps the counting
+// steps (profiles/r4s1_select_hist_ab.jsonl).  GMK_SELECT_HIST: 0 never, 1 the top byte
+// only, 2 both bytes; applied where the chain selects >= GMK_SELECT_HIST_NR ranks.
 #ifndef GMK_SELECT_HIST
-#define GMK_SELECT_HIST 0
+#define GMK_SELECT_HIST 2
+#endif
+#ifndef GMK_SELECT_HIST_NR
+#define GMK_SELECT_HIST_NR 2
 #endif
 
 // Candidate compaction (round 2).  Before step `bit` a chain's answer lies in
@@ -390,7 +397,7 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
           }
       }
     };
-    if constexpr (GMK_SELECT_HIST) {
+    if constexpr (GMK_SELECT_HIST >= 1 && NR >= GMK_SELECT_HIST_NR) {
       // bins of column c: buf(c, 0)[b * STR], b < 256 (the wave's own dead tile column)
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
@@ -458,7 +465,7 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
       finish_compacted(24);
       return;
     }
-    if constexpr (GMK_SELECT_HIST >= 2 && R >= 8) {
+    if constexpr (GMK_SELECT_HIST >= 2 && NR >= GMK_SELECT_HIST_NR && R >= 8) {
       // bits 23..16 from a second histogram per chain: the keys inside the chain's top-byte
       // bin, binned by their next byte (slots 256 q + b of column c's dead tile column)
 #pragma unroll
