@@ -328,5 +328,19 @@ r4s1n() {
   cut -c1-900 $O/c4_shard8.json
 }
 
+r4s1o() {
+  # round 4 session 1 closing set: GPU suite + smoke + the default bench line
+  # (tools/final_check.sh), then every BASELINE workload's line and the f3 timings
+  bash tools/final_check.sh || return $?
+  O=gpurun_out/r4s1o; mkdir -p $O
+  for w in "c2:--workload c2" "c5:--workload c5" "c5air:--workload c5 --reading aircomp" "c4:--workload c4 --steps 5 --warmup 1" "c4shard:--workload c4-shard"; do
+    n=${w%%:*}; a=${w#*:}
+    timeout -k 10 600 python -u bench.py $a > $O/bench_$n.json 2> $O/bench_$n.err || { tail -20 $O/bench_$n.err; return 2; }
+    cut -c1-300 $O/bench_$n.json
+  done
+  timeout -k 10 120 python -u tools/select_bench.py --K 1000 256 --reps 3 > $O/select.jsonl 2> $O/select.err || return 3
+  cat $O/select.jsonl
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
