@@ -574,13 +574,18 @@ def c5_check(groups, outs, reading, maxiter, recipe, per_group=3):
             X = Pn if Pn is not None else Xr
             ideal, _ = gm2_batched(X, {"maxiter": maxiter, "tol": 1e-5, "guess": g0})
             fin = torch.isfinite(out).all(dim=1)
-            rel = ((out - ideal).norm(dim=1) / ideal.norm(dim=1))[fin]
-            a = air.setdefault(str(var), {"problems": 0, "finite": 0, "rel_to_gm2": []})
+            rel_all = (out - ideal).norm(dim=1) / ideal.norm(dim=1)
+            # a trajectory that ran away can stay finite for a while: "stable" = finite and
+            # within half the GM's norm of it
+            stable = fin & (rel_all < 0.5)
+            a = air.setdefault(str(var), {"problems": 0, "finite": 0, "stable": 0,
+                                          "rel_to_gm2": []})
             a["problems"] += P
             a["finite"] += int(fin.sum())
-            a["rel_to_gm2"] += rel.tolist()
+            a["stable"] += int(stable.sum())
+            a["rel_to_gm2"] += rel_all[stable].tolist()
             if recipe == "outlier" or _c5_stable(var, X):
-                ok_air &= bool(fin.all())
+                ok_air &= bool(stable.all())
             continue
         for p in sorted({0, P // 2, P - 1})[:per_group]:
             if Pn is not None:
@@ -599,24 +604,37 @@ def c5_check(groups, outs, reading, maxiter, recipe, per_group=3):
     if air:
         out["aircomp_groups"] = {
             k: {"finite_frac": v["finite"] / v["problems"],
+                "stable_frac": v["stable"] / v["problems"],
                 "mean_rel_to_gm2": (sum(v["rel_to_gm2"]) / len(v["rel_to_gm2"])
                                     if v["rel_to_gm2"] else None),
                 "max_rel_to_gm2": max(v["rel_to_gm2"]) if v["rel_to_gm2"] else None,
-                "below_stability_bound": recipe == "caller" and _c5_stable(float(k), groups[0][5]
-                                                                           or groups[0][3])}
+                "noise_ratio_r": _c5_ratio(float(k), groups[0][5] or groups[0][3]),
+                "stable_regime": recipe == "caller" and _c5_stable(float(k), groups[0][5]
+                                                                   or groups[0][3])}
             for k, v in air.items()}
-        out["aircomp_what"] = ("AirComp gm groups: finite fraction over every problem, and "
-                               "||g_gm - g_gm2|| / ||g_gm2|| against the ideal GM of the same problem; "
-                               "the reference's gm is unstable above var ~ 0.02 at d = 100k "
-                               "(sqrt(var d / 2) > K / (sqrt(500) s), s = 0.07)")
+        out["aircomp_what"] = ("AirComp gm groups: over every problem the fraction finite and the "
+                               "fraction stable (finite and within 0.5 ||g_gm2|| of the ideal GM of "
+                               "the same problem), and ||g_gm - g_gm2|| / ||g_gm2|| over the stable "
+                               "ones.  The reference's gm adds column noise of norm ~ r d_k per "
+                               "iteration, r = sqrt(var d / 2) sqrt(500) s / K (s = 0.07, the model's "
+                               "RMS): stable at r = 0.22 (var 1e-3), marginal at 0.70 (1e-2: whether "
+                               "a trajectory runs away is decided by rounding), divergent at 2.2 "
+                               "(1e-1); `ok` requires every problem stable where r < 0.5 "
+                               "(DESIGN.md §3.6, tests/test_oracle_c5_stability.py)")
     return out
 
 
-def _c5_stable(var, X, s=0.07):
-    """The caller recipe's stability bound for the reference's gm: sqrt(var d / 2) below
-    K / (sqrt(500) s) (s = the model's RMS, 0.07)."""
+def _c5_ratio(var, X, s=0.07):
+    """The reference gm's noise ratio on the caller recipe: r = sqrt(var d / 2) sqrt(500) s / K
+    (s = the model's RMS, 0.07)."""
     K, d = (X.shape[1], X.shape[2]) if isinstance(X, torch.Tensor) else (X.K, X.d)
-    return math.sqrt(var * d / 2) < K / (math.sqrt(500.0) * s)
+    return math.sqrt(var * d / 2) * math.sqrt(500.0) * s / K
+
+
+def _c5_stable(var, X):
+    """Measured stable regime of the reference's gm on the caller recipe: r < 0.5 (r = 0.22
+    stable, 0.70 marginal)."""
+    return _c5_ratio(var, X) < 0.5
 
 
 def c5_cpu_baseline(X, g0, mean_iters, problems, budget):
