@@ -36,9 +36,14 @@ clean:
 # byzantine_aircomp_amd/libgmagg_alt.so; GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so
 # loads it at run time (tools/ab.py --variant alt=GMAGG_LIB=...).
 #   make alt ALT_FLAGS=-DGMK_H16_SHAPE=16
+# ALT_ONLY="resident resident_batched": recompile only those sources with ALT_FLAGS and
+# link the product's objects for the rest (the flags' macros live in those files).
 ALT       := byzantine_aircomp_amd/libgmagg_alt.so
 ALT_FLAGS ?= -DGMK_PIPE_VARIANT
-ALT_OBJS  := $(patsubst $(CSRC)/%.hip,$(BUILD)/alt/%.o,$(SRCS))
+ALT_ONLY  ?=
+ALT_SEL   := $(if $(ALT_ONLY),$(foreach n,$(ALT_ONLY),$(CSRC)/$(n).hip),$(SRCS))
+ALT_OBJS  := $(patsubst $(CSRC)/%.hip,$(BUILD)/alt/%.o,$(ALT_SEL)) \
+             $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(filter-out $(ALT_SEL),$(SRCS)))
 $(BUILD)/alt/gram.o: HIPFLAGS += -fno-slp-vectorize
 $(BUILD)/alt/%.o: $(CSRC)/%.hip $(HDRS) FORCE
 	@mkdir -p $(BUILD)/alt

@@ -97,19 +97,28 @@ unsigned checkin_need(unsigned blocks) {
   return blocks + ((e && atoi(e) != 0) ? 1u : 0u);
 }
 
-// XCD placement of the resident grids (read per call).  GMAGG_RES_XCD=1 (A/B, off): the
-// single-problem kernel's blocks all on one XCD when they fit its CUs (stride 8: only
-// blocks b % 8 == 0 work) — C2 172.8 vs 179.8 aggregations/s, kept off.  The batched
+// XCD placement of the resident grids (read per call).  The single-problem kernel's blocks
+// all on one XCD when they fit its CUs (stride 8: only blocks b % 8 == 0 work), its
+// granules stored so that they stay in that XCD's L2 (GMAGG_RES_XCD=2, the default):
+// C2 178.4 -> 227.3 aggregations/s (profiles/r4s2_xcd_local_ab.jsonl).  GMAGG_RES_XCD=1:
+// the same placement with agent-scope (L2-dropping) stores, 172.9; 0: neither.  The batched
 // kernel's groups are numbered XCD by XCD (GMAGG_RB_XCD=0 turns it off): a group of 49
 // blocks spans 2-3 XCDs instead of 8, the AirComp exchange's traffic 259 -> 110 GB per
 // 1024-problem launch, the prenoise sweep 70.5k -> 71.6k problems/s.
-unsigned res_xcd_stride(int nb, int num_cu) {
+// (local stores only when the check-in confirms from XCC_ID that every block is on one XCD:
+// resident.hip put_value; otherwise agent-scope stores, as for any placement)
+int res_xcd_mode() {
   const char* e = getenv("GMAGG_RES_XCD");
-  return (e && atoi(e) != 0 && nb <= num_cu / 8) ? 8u : 1u;
+  return e ? atoi(e) : 2;
 }
+unsigned res_xcd_stride(int nb, int num_cu) {
+  return (res_xcd_mode() != 0 && nb <= num_cu / 8) ? 8u : 1u;
+}
+// GMAGG_RB_XCD: 0 round-robin numbering, 1 XCD-major (default), 2 XCD-major with whole
+// groups per XCD whose granules stay in the XCD's L2 (resident_batched.hip rb_put)
 int rb_xcd_major() {
   const char* e = getenv("GMAGG_RB_XCD");
-  return (e && atoi(e) == 0) ? 0 : 1;     // on by default (round 4 A/B)
+  return e ? atoi(e) : 1;                 // 1 by default (round 4 A/B)
 }
 
 // Stream-orders the context's workspace between calls (see gm_ctx::ws_ev): the
@@ -349,6 +358,7 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   a.checkin = a.gran + (size_t)2 * nb * S;      // (resident_gran_words: + nb + 1 slots)
   a.need = checkin_need((unsigned)nb);
   a.stride = res_xcd_stride(nb, c->num_cu);
+  a.local = a.stride == 8 && res_xcd_mode() == 2;
   a.bar = bar; a.st = w.st;
   hipEvent_t e0, e1;
   rc = record_pass_begin(c, s, &e0, &e1);
@@ -361,6 +371,10 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   unsigned hbar[4] = {0, 0, 0, 0};
   HIPCHK(hipMemcpyAsync(hbar, bar, 16, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  static const bool verbose = getenv("GMAGG_RES_VERBOSE") != nullptr;
+  if (verbose)
+    fprintf(stderr, "gmagg resident: nb=%d stride=%u local=%d (requested %d) timed_out=%u\n", nb,
+            a.stride, hbar[0] ? (int)hbar[0] - 1 : -1, a.local, hbar[2]);
   if (hbar[2]) {   // the grid was not co-resident long enough: caller reruns on streaming
     *timed_out = true;
     if (!hbar[3]) c->res_skip = kResSkipAfterCheckinFail;   // failed at the check-in
@@ -403,7 +417,8 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
   const int64_t pbytes = panels ? (d + Wp - 1) / Wp * ldx * 4 : K * ldx * 4;
   if (pbytes >= ((int64_t)1 << 31)) return kRbNotTaken;
   RbPlan plan{};
-  if (!rb_plan(K, d, P, o->mode, c->num_cu, &plan)) return kRbNotTaken;
+  const int xcd = rb_xcd_major();
+  if (!rb_plan(K, d, P, o->mode, c->num_cu, &plan, xcd == 2)) return kRbNotTaken;
 
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t r0 = off; off = align_up(off + bytes, 256); return r0; };
@@ -445,7 +460,8 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
   a.flag = flag;
   a.checkin = reinterpret_cast<unsigned long long*>(b + o_ci);
   a.need = checkin_need(nblocks);
-  a.xcd_major = rb_xcd_major();
+  a.xcd_major = xcd != 0;
+  a.local = xcd == 2;
   a.st = st;
   hipEvent_t e0, e1;
   rc = record_pass_begin(c, s, &e0, &e1);
@@ -458,6 +474,10 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
   HIPCHK(hipMemcpyAsync(hst, st, sizeof(KState) * P, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(hflag, flag, 16, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  static const bool verbose = getenv("GMAGG_RES_VERBOSE") != nullptr;
+  if (verbose)
+    fprintf(stderr, "gmagg resident_batched: ng=%d nb=%d xcd=%d local_groups=%u timed_out=%u\n",
+            plan.ng, plan.nb, xcd, hflag[1], hflag[0]);
   if (hflag[0]) {
     if (c->timing && !c->ev_used.empty()) {
       c->ev_free.push_back(c->ev_used.back().first);

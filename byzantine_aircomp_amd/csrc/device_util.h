@@ -251,27 +251,40 @@ __device__ __forceinline__ float xlane_wave_sum_f32(float v) {
 constexpr unsigned kCheckinTag = 0xC0DEC0DEu;
 constexpr uint64_t kCheckinTicks = 10000000ull;   // 100 ms
 
+// The XCD this wave runs on (0-7): hardware register XCC_ID.
+__device__ __forceinline__ unsigned xcc_id() {
+  return __builtin_amdgcn_s_getreg(20 | (0 << 6) | ((4 - 1) << 11)) & 7u;   // hwreg(XCC_ID, 0, 4)
+}
+
+// s_same (optional): every slot in [same_lo, same_hi) carries this block's XCD (each block
+// writes xcc_id() + 1 into its slot's low word), i.e. those blocks share one L2; read from
+// the same slots by every block of the range, so the range's blocks agree on it.
 __device__ __forceinline__ bool grid_checkin(unsigned long long* ci, unsigned slot, unsigned need,
                                              unsigned* tmo_word, unsigned* passed,
-                                             uint64_t ticks, int* s_ok) {
+                                             uint64_t ticks, int* s_ok, int* s_same = nullptr,
+                                             unsigned same_lo = 0, unsigned same_hi = 0) {
   typedef __attribute__((address_space(1))) unsigned long long gu64_t;
   typedef __attribute__((address_space(1))) unsigned gu32_t;
   gu64_t* c = (gu64_t*)ci;
   gu32_t* tmo = (gu32_t*)tmo_word;
   const unsigned tid = threadIdx.x;
+  const unsigned mine = xcc_id() + 1u;
   if (tid == 0) {
     *s_ok = 1;
-    __hip_atomic_store(c + slot, (unsigned long long)kCheckinTag << 32, __ATOMIC_RELAXED,
+    if (s_same) *s_same = 1;
+    __hip_atomic_store(c + slot, ((unsigned long long)kCheckinTag << 32) | mine, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  bool ok = true;
+  bool ok = true, same = true;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (unsigned b = tid; ok && b < need; b += blockDim.x) {
     for (unsigned spins = 0;; ++spins) {
-      if ((unsigned)(__hip_atomic_load(c + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) ==
-          kCheckinTag)
+      const unsigned long long v = __hip_atomic_load(c + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((unsigned)(v >> 32) == kCheckinTag) {
+        if (b >= same_lo && b < same_hi && (unsigned)v != mine) same = false;
         break;
+      }
       __builtin_amdgcn_s_sleep(2);
       if (((spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > ticks) ||
           __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -282,6 +295,7 @@ __device__ __forceinline__ bool grid_checkin(unsigned long long* ci, unsigned sl
     }
   }
   if (!ok) *s_ok = 0;
+  if (!same && s_same) *s_same = 0;
   __syncthreads();
   if (tid == 0 && *s_ok && __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
     *s_ok = 0;                       // every slot written, but the grid already gave up

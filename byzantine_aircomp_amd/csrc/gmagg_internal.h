@@ -123,6 +123,9 @@ struct ResArgs {
   // block b / 8), so that — workgroups being dispatched round-robin over the 8 XCDs — every
   // working block sits on ONE XCD and the exchange stays inside its L2 (A/B knob)
   unsigned stride;
+  // 1: when the check-in finds every block on one XCD, the granules are stored so that
+  // they stay in that XCD's L2 (resident.hip put_value); 0: agent-scope stores always
+  int local;
   KState* st;
 };
 // Plan a resident launch over nch chunks: chunks per block and blocks (false: the
@@ -160,6 +163,9 @@ struct ResBArgs {
   // XCD-major: logical blocks numbered XCD by XCD (b % 8 first), so a group of NB blocks
   // spans ceil(NB / 32) + 1 XCDs instead of 8 (A/B knob)
   int xcd_major;
+  // 1: groups whose blocks the check-in finds on one XCD store their granules into that
+  // XCD's L2 (resident_batched.hip rb_put); the plan then gives each XCD whole groups
+  int local;
   KState* st;             // [P]
 };
 struct RbPlan {
@@ -168,7 +174,10 @@ struct RbPlan {
   int ng;                 // problems in flight (groups)
   int mode;               // gm_mode (the kernel is built per mode)
 };
-bool rb_plan(int64_t K, int64_t d, int64_t P, int mode, int num_cu, RbPlan* plan);
+// xcd_whole: whole groups per XCD (8 x floor(cap / 8 / nb) groups, when that is >= 8), so
+// that each group's blocks share one L2 (GMAGG_RB_XCD=2)
+bool rb_plan(int64_t K, int64_t d, int64_t P, int mode, int num_cu, RbPlan* plan,
+             bool xcd_whole = false);
 size_t rb_gran_words(int64_t K, const RbPlan& plan);
 hipError_t launch_resident_batched(const RbPlan& plan, const ResBArgs& a, bool coop, hipStream_t s);
 

@@ -75,9 +75,15 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 // sum rounded once to fp32 (relative 6e-8; the reference's own norms are fp32
 // sums, M:174/M:180), the sum over blocks is fp64.  Half the granules of an fp64
 // {hi, lo} pair: the poll traffic on those lines is what the exchange costs.
-__device__ __forceinline__ void put_value(gu64* g, unsigned tag, float v) {
-  __hip_atomic_store(g, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+// `local` (every block of the grid on ONE XCD, checked at check-in from XCC_ID): the
+// store keeps the line in that XCD's L2 (workgroup scope: `sc0`), where the readers'
+// `sc1` polls are served; an agent-scope (`sc1`) store drops it from the L2, so a
+// same-XCD reader fetches it at the cross-XCD rate (MI355X_MICROARCH.md, store flavours).
+// A granule is one 8-byte store either way (tag and value never torn apart).
+__device__ __forceinline__ void put_value(gu64* g, unsigned tag, float v, bool local = false) {
+  const unsigned long long x = ((unsigned long long)tag << 32) | __float_as_uint(v);
+  if (local) __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Sum over blocks b = g, g + G, g + 2G, ... (< nb, in that order) of one value of
@@ -86,7 +92,13 @@ __device__ __forceinline__ void put_value(gu64* g, unsigned tag, float v) {
 // (s_memrealtime): on timeout (a time-sliced GPU, blocks not co-resident) the
 // flag tmo is raised and every block gives up; the host then reruns the problem
 // on the streaming path.
-constexpr int kNbChunk = 4;
+#ifndef GMK_RES_FASTCOEF
+#define GMK_RES_FASTCOEF 0  // A/B knob: the AirComp coefficients on v_rcp / v_rsq (1 ulp)
+#endif
+#ifndef GMK_RES_NBCHUNK
+#define GMK_RES_NBCHUNK 4   // A/B knob: >= nb gives one load round trip and one stage (G = 1)
+#endif
+constexpr int kNbChunk = GMK_RES_NBCHUNK;
 
 __device__ __forceinline__ bool gather_value(const gu64* g, int64_t bstride, unsigned b_first,
                                              unsigned b_step, unsigned nb, unsigned tag,
@@ -169,7 +181,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   __shared__ double s_part[NW * 64];
   __shared__ double scratch[16];
   __shared__ float s_anoise;
-  __shared__ int s_ok;
+  __shared__ int s_ok, s_same;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -186,7 +198,12 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   gu64* gran = (gu64*)a.gran;                      // [2][nb][2 NV]
   gu32* tmo = (gu32*)a.bar + 2;
   // every block of the grid co-resident before anything is read (device_util.h)
-  if (!grid_checkin(a.checkin, bid, a.need, a.bar + 2, a.bar + 3, kCheckinTicks, &s_ok)) return;
+  if (!grid_checkin(a.checkin, bid, a.need, a.bar + 2, a.bar + 3, kCheckinTicks, &s_ok, &s_same,
+                    0u, nb))
+    return;
+  const bool local = a.local && s_same;            // identical in every block (same slots)
+  if (bid == 0 && tid == 0)                        // reported to the host (bar[0]: 1 + local)
+    __hip_atomic_store((gu32*)a.bar, 1u + (unsigned)local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   // ---- the block's tiles: loaded once, resident for the whole call
   float x[CPB][R][V];
@@ -219,8 +236,8 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
       for (int m = 0; m < RPL; ++m) {
         const int64_t k = rg + (int64_t)NRG * (i_c + m);
         if (k < K) {
-          put_value(out + k, tag, (float)racc[m]);
-          if (racc2) put_value(out + K + k, tag, (float)racc2[m]);
+          put_value(out + k, tag, (float)racc[m], local);
+          if (racc2) put_value(out + K + k, tag, (float)racc2[m], local);
         }
       }
     }
@@ -230,8 +247,8 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         m += s_fin[0][ww];
         g += s_fin[1][ww];
       }
-      put_value(out + 2 * K, tag, (float)m);
-      put_value(out + 2 * K + 1, tag, (float)g);
+      put_value(out + 2 * K, tag, (float)m, local);
+      put_value(out + 2 * K + 1, tag, (float)g, local);
     }
   };
   // wave partials of the movement and ||g||^2 -> s_fin (read by publish after a
@@ -386,6 +403,38 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
           const double W = xlane_wave_sum(wk);
           if (kv) s_coef[k] = (float)(wk / W);
           if (lane == 0) s_anoise = 0.f;
+        } else if (GMK_RES_FASTCOEF) {
+          // the same steps with the hardware reciprocal / reciprocal square root (1 ulp)
+          // and fp32 square roots, off the iteration's dependent chain's slow sequences
+          const float s = sqrtf((float)(s_wp[1] * (1.0 / (double)d)));      // M:146
+          const float thr = (s * s) * 500.0f;                                  // M:152
+          float ck = 0.f;
+          if (kv) {
+            float h2;
+            if (pre_h2) {
+              h2 = s_h2[k];
+            } else {
+              float n4[4];
+              normal4(a.seed, kStreamChannel, (uint64_t)it, (uint64_t)k, n4);
+              const float hr = n4[0] * 0.70710678118654752f, hi = n4[1] * 0.70710678118654752f;
+              h2 = hr * hr + hi * hi;                                          // M:403
+            }
+            const float d0 = sqrtf((float)s_d2[k]);
+            const float dist = d0 != d0 ? d0 : fmaxf(d0, a.eps);
+            const float rd = __builtin_amdgcn_rcpf(dist);
+            const float pk = ((float)s_r[k] + s * s) *
+                             __builtin_amdgcn_rcpf(dist * dist * (float)(d + 1) * h2);  // M:404
+            const float pup = pk != pk ? pk : fmaxf(pk, thr);                   // M:405
+            ck = sqrtf((float)a.P_max) * __builtin_amdgcn_rsqf(pup) * rd;       // M:407
+          }
+          const float Sc = xlane_wave_sum_f32(ck);                             // fp32, as M:153
+          const float nd = !a.has_noise ? 0.f
+                           : (float)a.noise_sd * (pre_h2 ? s_nd
+                                                         : normal1(a.seed, kStreamNoise,
+                                                                   (uint64_t)it, (uint64_t)d));
+          const float scale = s * __builtin_amdgcn_rcpf(s * Sc + nd);          // M:153-155
+          if (kv) s_coef[k] = ck * scale;
+          if (lane == 0) s_anoise = a.has_noise ? scale * (float)a.noise_sd : 0.f;
         } else {
           const float s = sqrtf((float)(s_wp[1] / (double)d));      // M:146
           const float thr = (s * s) * 500.0f;                         // M:152

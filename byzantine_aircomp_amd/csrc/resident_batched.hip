@@ -61,9 +61,13 @@ constexpr int kRbChunk = 8;                      // granules in flight per poll 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 
-__device__ __forceinline__ void rb_put(gu64* g, unsigned tag, float v) {
-  __hip_atomic_store(g, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+// `local`: every block of the group on one XCD (checked at check-in): the granule stays in
+// that XCD's L2 (workgroup-scope store, `sc0`) for the group's `sc1` polls (resident.hip
+// put_value)
+__device__ __forceinline__ void rb_put(gu64* g, unsigned tag, float v, bool local) {
+  const unsigned long long x = ((unsigned long long)tag << 32) | __float_as_uint(v);
+  if (local) __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Sum over blocks b = first, first + step, ... < nb of the value at g + b * bstride of
@@ -176,7 +180,7 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   __shared__ double s_part[NT];
   __shared__ float s_rk[MODE == 1 ? NW : 1][64];   // gm: lane k's ||x_k||^2, each wave's copy
   __shared__ float s_an;
-  __shared__ int s_ok;
+  __shared__ int s_ok, s_same;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -207,8 +211,14 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   if (tid < NW * KC) (&s_coef[0][0])[tid] = 0.f;
   // every block of the grid co-resident before any problem's X is read or (pre-noise)
   // written: a grid that is not fails here with X untouched (device_util.h)
-  if (!grid_checkin(a.checkin, blockIdx.x, a.need, a.flag, a.flag + 2, kCheckinTicks, &s_ok))
+  // (slot = logical block: a group's slots are contiguous, so the check-in also tells
+  // whether the whole group shares one XCD)
+  if (!grid_checkin(a.checkin, (unsigned)lb, a.need, a.flag, a.flag + 2, kCheckinTicks, &s_ok,
+                    &s_same, (unsigned)(grp * NB), (unsigned)(grp * NB + NB)))
     return;
+  const bool local = a.local && s_same;            // identical in the group's blocks
+  if (local && bi == 0 && tid == 0)                // groups on one XCD, counted for the host
+    __hip_atomic_fetch_add((gu32*)a.flag + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   f4 x[KV > 0 ? KV : 1];   // the tile's register rows: row k of the thread's 4 columns
   float g[4];              // the iterate at those columns
@@ -233,14 +243,14 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
       double sm = 0.0;
 #pragma unroll
       for (int ww = 0; ww < NW; ++ww) sm += (double)s_rows[pb][ww][tid];
-      rb_put(out + tid, tag, (float)sm);
+      rb_put(out + tid, tag, (float)sm, local);
     }
     if (with_r && tid >= 64 && tid < 64 + K) {
       const int k = tid - 64;
       double sm = 0.0;
 #pragma unroll
       for (int ww = 0; ww < NW; ++ww) sm += (double)s_rows2[ww][k];
-      rb_put(out + K + k, tag, (float)sm);
+      rb_put(out + K + k, tag, (float)sm, local);
     }
     if (tid == 128) {
       double m = 0.0, gg = 0.0;
@@ -249,8 +259,8 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
         m += (double)s_fin[pb][0][ww];
         gg += (double)s_fin[pb][1][ww];
       }
-      rb_put(out + 2 * K, tag, (float)m);
-      rb_put(out + 2 * K + 1, tag, (float)gg);
+      rb_put(out + 2 * K, tag, (float)m, local);
+      rb_put(out + 2 * K + 1, tag, (float)gg, local);
     }
   };
   auto wave_fin = [&](float mv, float gn) {
@@ -668,7 +678,7 @@ static const void* rb_kernel(int kr, int mode) {
 
 int rb_rows_for(int64_t K) { return K <= 16 ? 16 : K <= 32 ? 32 : K <= 50 ? 50 : K <= 52 ? 52 : 0; }
 
-bool rb_plan(int64_t K, int64_t d, int64_t P, int mode, int num_cu, RbPlan* plan) {
+bool rb_plan(int64_t K, int64_t d, int64_t P, int mode, int num_cu, RbPlan* plan, bool xcd_whole) {
   int kr = rb_rows_for(K);
   // GMAGG_RB_ROWS=52: the 36 + 16-row tile for K <= 50 too (A/B of the row split)
   static const int force = getenv("GMAGG_RB_ROWS") ? atoi(getenv("GMAGG_RB_ROWS")) : 0;
@@ -688,6 +698,7 @@ bool rb_plan(int64_t K, int64_t d, int64_t P, int mode, int num_cu, RbPlan* plan
   plan->mode = mode;
   plan->nb = (int)nb;
   plan->ng = (int)std::min<int64_t>(P, cap / nb);
+  if (xcd_whole && cap / 8 / nb >= 1) plan->ng = (int)std::min<int64_t>(P, 8 * (cap / 8 / nb));
   return true;
 }
 

@@ -684,3 +684,26 @@ def iteration_cases():
     cases.append(("c4like_256x2^20_s4040_shift", lambda: c4_like(256, 1 << 20, seed=4040,
                                                                  shift=0.07, flag=("windowed",))))
     return cases
+
+
+@pytest.mark.parametrize("agg", ["gm2", "gm"])
+def test_resident_xcd_local_exchange_matches_agent_scope(agg, monkeypatch):
+    """C2's single-problem resident kernel: its 31 blocks on one XCD with the granules kept
+    in that XCD's L2 (GMAGG_RES_XCD=2, the default; resident.hip put_value) against the
+    blocks dealt over every XCD with agent-scope granule stores (GMAGG_RES_XCD=0).  The
+    exchange carries the same values in the same order, only where they are cached
+    differs, so the results are bit-identical."""
+    X, p = _sgd_like(50, 7850, 2718)
+    X, p = X.cuda(), p.cuda()
+    opts = {"maxiter": 1000, "tol": 1e-5, "guess": p}
+    if agg == "gm":
+        opts.update(maxiter=200, noise_var=1e-2, seed=5)
+    f = getattr(bz(), agg)
+    outs = {}
+    for mode in ("2", "0"):
+        monkeypatch.setenv("GMAGG_RES_XCD", mode)
+        outs[mode] = (f(X.clone(), dict(opts)).cpu(), bz().aggregators.last_result)
+    (a, ra), (b, rb) = outs["2"], outs["0"]
+    assert ra.algo == "resident" and rb.algo == "resident"
+    assert ra.iters == rb.iters
+    assert torch.equal(a, b)

@@ -342,5 +342,80 @@ r4s1o() {
   cat $O/select.jsonl
 }
 
+r4s2a() {
+  # C2's single resident kernel with every block on one XCD AND the granules stored so that
+  # they stay in that XCD's L2 (GMAGG_RES_XCD=2; the check-in confirms the placement from
+  # XCC_ID, else agent-scope stores) against the default placement and the one-XCD placement
+  # with agent-scope stores (=1, round 4: slower); parity of the resident tests first
+  O=gpurun_out/r4s2a; mkdir -p $O
+  GMAGG_RES_XCD=2 GMAGG_RES_VERBOSE=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_weiszfeld.py tests/test_gpu_distributed.py -k "resident or gm_host or philox or gm2_matches or clamp" > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log; grep -c "local=1" $O/t.log; grep -c "local=0" $O/t.log
+  GMAGG_RES_XCD=2 GMAGG_RES_VERBOSE=1 timeout -k 10 200 python -u bench.py --workload c2 --no-cpu --alt-steps 0 --soak 0 --steps 3 --warmup 1 > $O/c2_local.json 2> $O/c2_local.err || { tail -20 $O/c2_local.err; return 2; }
+  sort $O/c2_local.err | uniq -c | head -5; cut -c1-400 $O/c2_local.json
+  timeout -k 10 600 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant base= --variant xcd1=GMAGG_RES_XCD=1 --variant local=GMAGG_RES_XCD=2 --out $O/ab_c2.jsonl > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; return 3; }
+  tail -4 $O/ab_c2.log
+}
+
+r4s2b() {
+  # C5: whole groups per XCD with their granules kept in the XCD's L2 (GMAGG_RB_XCD=2)
+  # against the XCD-major numbering (default, groups span 2-3 XCDs); parity first
+  O=gpurun_out/r4s2b; mkdir -p $O
+  GMAGG_RB_XCD=2 GMAGG_RES_VERBOSE=1 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_resident_batched.py tests/test_gpu_c5_fullsize.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log; grep "resident_batched:" $O/t.log | sort | uniq -c | sort -rn | head -5
+  GMAGG_RB_XCD=2 GMAGG_RES_VERBOSE=1 timeout -k 10 300 python -u bench.py --workload c5 --reading aircomp --no-cpu --alt-steps 0 --soak 0 --steps 1 --warmup 0 > $O/c5air_local.json 2> $O/c5air_local.err || { tail -20 $O/c5air_local.err; return 2; }
+  sort $O/c5air_local.err | uniq -c | head -5; cut -c1-300 $O/c5air_local.json
+  timeout -k 10 900 python -u tools/ab.py --rounds 2 --bench=--workload,c5,--reading,aircomp,--no-cpu,--alt-steps,0,--soak,0,--no-check,--steps,1,--warmup,0 --variant base= --variant local=GMAGG_RB_XCD=2 --out $O/ab_c5air.jsonl > $O/ab_c5air.log 2>&1 || { tail -20 $O/ab_c5air.log; return 3; }
+  tail -3 $O/ab_c5air.log
+  timeout -k 10 600 python -u tools/ab.py --rounds 3 --bench=--workload,c5,--no-cpu,--alt-steps,0,--soak,0,--no-check --variant base= --variant local=GMAGG_RB_XCD=2 --out $O/ab_c5.jsonl > $O/ab_c5.log 2>&1 || { tail -20 $O/ab_c5.log; return 4; }
+  tail -3 $O/ab_c5.log
+}
+
+r4s2c() {
+  # C2 after the XCD-local exchange became the default: its exchange floor (libgmagg_alt.so
+  # built with ALT_FLAGS=-DGMK_RES_DBG=7) in both exchange modes, the product at tol -1
+  # (1000 iterations, same box), the resident / single-problem GPU tests, the kernel trace
+  O=gpurun_out/r4s2c; mkdir -p $O
+  B="--no-cpu --no-check --alt-steps 0 --soak 0"
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_weiszfeld.py tests/test_gpu_training.py tests/test_gpu_distributed.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  for m in 2 0; do
+    GMAGG_RES_XCD=$m GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so timeout -k 10 200 python -u bench.py --workload c2 --tol -1 --steps 5 $B > $O/c2_exchange_only_x$m.json 2> $O/c2x$m.err || return 2
+    GMAGG_RES_XCD=$m timeout -k 10 200 python -u bench.py --workload c2 --tol -1 --steps 5 $B > $O/c2_tolneg_x$m.json 2> $O/c2_x$m.err || return 3
+  done
+  for f in $O/c2_*.json; do echo "$f $(python -c "import json,sys;l=json.load(open('$f'));print(l['ms_per_step'])")"; done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c2 -o t -- python3 bench.py --workload c2 --no-cpu --alt-steps 0 --soak 0 > $O/trace_c2.log 2>&1 || return 4
+  head -4 $O/trace_c2/t_kernel_stats.csv
+  timeout -k 10 200 python -u bench.py --workload c2 > $O/bench_c2.json 2> $O/bench_c2.err || { tail -20 $O/bench_c2.err; return 5; }
+  cut -c1-600 $O/bench_c2.json
+}
+
+r4s2d() {
+  # C2 per-phase time of one iteration (block 0, s_memrealtime; libgmagg_alt.so built with
+  # ALT_FLAGS=-DGMK_RES_PROF) with the XCD-local exchange (2) and the agent-scope one (0);
+  # the local-vs-agent bit-identity test
+  O=gpurun_out/r4s2d; mkdir -p $O
+  timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_weiszfeld.py -k xcd_local > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  for m in 2 0; do
+    GMAGG_RES_XCD=$m GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so timeout -k 10 200 python -u bench.py --workload c2 --tol -1 --steps 2 --warmup 1 --no-cpu --no-check --alt-steps 0 --soak 0 > $O/prof_x$m.json 2> $O/prof_x$m.err || return 2
+    echo "mode $m"; grep GMK_RES_PROF $O/prof_x$m.err | tail -2
+  done
+}
+
+r4s2e() {
+  # C2 after the XCD-local exchange: the AirComp coefficients on v_rcp / v_rsq (fc:
+  # libgmagg_alt_fc.so, -DGMK_RES_FASTCOEF=1), the gather in one round trip and one stage
+  # (g1: libgmagg_alt_g1.so, -DGMK_RES_NBCHUNK=32), both (libgmagg_alt.so); parity of the
+  # single-problem GPU tests on each, then interleaved A/B
+  O=gpurun_out/r4s2e; mkdir -p $O
+  for v in fc g1 ""; do
+    L=byzantine_aircomp_amd/libgmagg_alt${v:+_$v}.so
+    GMAGG_LIB=$L timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_weiszfeld.py > $O/t_$v.log 2>&1 || { tail -30 $O/t_$v.log; return 1; }
+    echo "$L: $(tail -1 $O/t_$v.log)"
+  done
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant base= --variant fc=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_fc.so --variant g1=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_g1.so --variant both=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so --out $O/ab_c2.jsonl > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; return 2; }
+  tail -5 $O/ab_c2.log
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
