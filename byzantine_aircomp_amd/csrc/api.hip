@@ -334,7 +334,8 @@ int record_pass_end(gm_ctx* c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
 // iteration on the device.
 int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
                  const float* guess0, float* out, const gm_opts* o, gm_result* res,
-                 const PassCfg& cfg, int cpb, int nb, hipStream_t s, bool* timed_out) {
+                 const PassCfg& cfg, int cpb, int nb, hipStream_t s, bool* timed_out,
+                 int64_t pstride = 0, int wshift = 0) {
   *timed_out = false;
   // granules [2][nb][2 values] in the slab region, + the timeout word in sums
   const size_t words = resident_gran_words(K, cfg, nb);
@@ -350,6 +351,7 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   HIPCHK(hipMemsetAsync(w.slab, 0, align_up(words * 8, 16), s));   // every tag = 0
   ResArgs a{};
   a.X = X; a.K = K; a.d = d; a.ldx = ldx; a.guess0 = guess0; a.out = out;
+  a.pstride = pstride; a.wshift = wshift;
   a.maxiter = o->maxiter; a.tol = (float)o->tol; a.eps = (float)o->eps;
   a.mode = o->mode; a.has_noise = o->mode == GM_MODE_AIRCOMP && o->has_noise;
   a.P_max = o->P_max; a.noise_sd = std::sqrt(std::max(0.0, o->noise_var) / 2.0);
@@ -825,9 +827,32 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       panel_gram_rejected = true;
       algo = GM_ALGO_STREAM;
     }
-    // One problem that fits on chip (K <= 52; gm at K <= 50): the batched register-resident
-    // kernel with P = 1 reads the panels once for all iterations (the C2 kernel takes rows
-    // only).  Same eligibility as the batched call; the fused pre-noise included.
+    // One problem that fits on chip: the single-problem resident kernel (C2's, reading the
+    // panels with its rows tile: V = 2 columns per lane, within one panel) when its grid
+    // fits one XCD (the L2-kept exchange, §3.3: C2's shape 4.3 ms there against 6.7 ms on
+    // the batched kernel's 4 blocks), else the batched kernel with P = 1 (K <= 52; gm at
+    // K <= 50; the fused pre-noise included).  Either reads the panels once for all
+    // iterations.
+    const bool host_noise = o->mode == GM_MODE_AIRCOMP && o->noise_source == GM_NOISE_HOST;
+    if ((algo == GM_ALGO_AUTO || algo == GM_ALGO_RESIDENT) && !sharded && !c->comm && !c->ar_fn &&
+        !host_noise && K <= 64 && resident_allowed(c)) {
+      PassCfg rcfg{};
+      int cpb = 0, nbr = 0;
+      int ws = 0;
+      while (((int64_t)1 << ws) < W) ++ws;
+      if (pick_cfg(K, 2, W, &rcfg) && W % rcfg.V == 0 &&
+          resident_plan(rcfg, (d + rcfg.LPR * rcfg.V - 1) / (rcfg.LPR * rcfg.V), c->num_cu, &cpb,
+                        &nbr) &&
+          res_xcd_stride(nbr, c->num_cu) == 8) {
+        bool timed_out = false;
+        int rco = apply_oma();
+        if (rco) return rco;
+        const int rc0 = run_resident(c, X, K, d, K * W, guess0, out, o, res, rcfg, cpb, nbr, s,
+                                     &timed_out, ldx, ws);
+        if (rc0 || !timed_out) return rc0;
+        algo = GM_ALGO_STREAM;   // the X noised above: stream (no second pre-noise)
+      }
+    }
     if ((algo == GM_ALGO_AUTO || algo == GM_ALGO_RESIDENT) && !sharded && !c->comm && !c->ar_fn) {
       const int rc0 = run_resident_batched(c, X, 1, K, d, ldx, (d + W - 1) / W * ldx, true, W,
                                            guess0, d, out, d, o, res, s);

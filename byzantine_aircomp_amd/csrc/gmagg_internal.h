@@ -108,6 +108,10 @@ hipError_t launch_batched_finalize(const float* g0, const float* g1, int64_t d, 
 struct ResArgs {
   const float* X;
   int64_t K, d, ldx;
+  // panels (pstride > 0): element (k, j) at X + (j >> wshift) * pstride + k * 2^wshift +
+  // (j & (2^wshift - 1)); rows [K][ldx] otherwise
+  int64_t pstride;
+  int wshift;
   const float* guess0;
   float* out;
   int64_t maxiter;

@@ -92,11 +92,17 @@ __device__ __forceinline__ void put_value(gu64* g, unsigned tag, float v, bool l
 // (s_memrealtime): on timeout (a time-sliced GPU, blocks not co-resident) the
 // flag tmo is raised and every block gives up; the host then reruns the problem
 // on the streaming path.
+// The AirComp coefficients (K <= 64) on v_rcp / v_rsq (1 ulp) and fp32 square roots
+// instead of IEEE divisions and fp64 square roots on the iteration's dependent chain: C2
+// 228.4 -> 234.5 aggregations/s (profiles/r4s2_c2_coef_gather_ab.jsonl); 0 = the exact
+// sequence (A/B knob)
 #ifndef GMK_RES_FASTCOEF
-#define GMK_RES_FASTCOEF 0  // A/B knob: the AirComp coefficients on v_rcp / v_rsq (1 ulp)
+#define GMK_RES_FASTCOEF 1
 #endif
+// Granules per poll round trip.  32 (>= C2's 31 blocks: one round trip, one stage, G = 1)
+// spilled 336 bytes and measured 4x slower (55.9 aggregations/s, same A/B)
 #ifndef GMK_RES_NBCHUNK
-#define GMK_RES_NBCHUNK 4   // A/B knob: >= nb gives one load round trip and one stage (G = 1)
+#define GMK_RES_NBCHUNK 4
 #endif
 constexpr int kNbChunk = GMK_RES_NBCHUNK;
 
@@ -211,11 +217,24 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   for (int h = 0; h < CPB; ++h) {
     const int64_t col = (ch0 + h) * J + (int64_t)c * V;
     const bool cval = col < d;
+    if (a.pstride == 0) {
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const int64_t k = rg + (int64_t)NRG * i;
+      for (int i = 0; i < R; ++i) {
+        const int64_t k = rg + (int64_t)NRG * i;
 #pragma unroll
-      for (int v = 0; v < V; ++v) x[h][i][v] = (cval && k < K) ? a.X[k * a.ldx + col + v] : 0.f;
+        for (int v = 0; v < V; ++v) x[h][i][v] = (cval && k < K) ? a.X[k * a.ldx + col + v] : 0.f;
+      }
+    } else {
+      // panels: the V columns of a lane lie in one panel (V divides its width); the last
+      // panel's padding past d is never read
+      const int64_t W = (int64_t)1 << a.wshift;
+      const float* pc = a.X + (col >> a.wshift) * a.pstride + (col & (W - 1));
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int64_t k = rg + (int64_t)NRG * i;
+#pragma unroll
+        for (int v = 0; v < V; ++v) x[h][i][v] = (cval && col + v < d && k < K) ? pc[k * W + v] : 0.f;
+      }
     }
   }
   float gcur = fin ? a.guess0[gj] : 0.f;       // finisher thread: the iterate at column gj

@@ -44,6 +44,9 @@ constexpr int kRbCols = 2048;                    // columns per block
 // GMK_RB_PREFETCH_ROWS = n > 0: during iteration it of problem p, the rows
 // [n·it, n·it + n) of the group's NEXT problem are read into a junk LDS line (LDS-DMA, no
 // registers), so that the next tile load finds them in the Infinity Cache (A/B)
+#ifndef GMK_RB_NZ4
+#define GMK_RB_NZ4 0   // timing probe only (changes the draws): see draw_pass
+#endif
 #ifndef GMK_RB_PREFETCH_ROWS
 #define GMK_RB_PREFETCH_ROWS 0
 #endif
@@ -437,11 +440,20 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
           h2k = hr * hr + hi * hi;
         }
         if (a.has_noise) {
+#if GMK_RB_NZ4
+          // (timing probe: one Philox block per 4 columns, element j = normal j & 3 of
+          // block j >> 2; NOT the keying of the other paths)
+          float zd[4];
+          normal4_hw(seed_p, kStreamNoise, (uint64_t)i, (uint64_t)d >> 2, zd);
+          ndr = zd[d & 3];
+          normal4_hw(seed_p, kStreamNoise, (uint64_t)i, (uint64_t)col0 >> 2, nz);
+#else
           ndr = normal1(seed_p, kStreamNoise, (uint64_t)i, (uint64_t)d);
           sfor<0, 4>([&](auto v) {
             nz[v] = normal1(seed_p, kStreamNoise, (uint64_t)i, (uint64_t)(col0 + v));
             __builtin_amdgcn_sched_barrier(0);
           });
+#endif
         }
       }
     };

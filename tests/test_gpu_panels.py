@@ -102,14 +102,20 @@ def test_panels_store_rows_and_default_guess():
 
 
 def test_panels_reject_non_streaming_algos():
-    """Panels run the streaming pass, (gm2, K <= 256) the f16 Gram or (K <= 52) the batched
-    resident kernel; the other algorithms, the f32 Gram, Gram for AirComp gm or K > 256,
-    and "resident" at K = 64 raise."""
+    """Panels run the streaming pass, (gm2, K <= 256) the f16 Gram or a resident kernel
+    (K <= 64 on a grid that fits one XCD: C2's; else K <= 52: the batched one); the other
+    algorithms, the f32 Gram, Gram for AirComp gm or K > 256, and "resident" at K = 65
+    raise.  At K = 64 and a small d "resident" runs C2's kernel."""
     X, g0 = _data(64, 512, seed=1)
     P = bz().ClientPanels.from_rows(X)
-    for algo in ("twopass", "resident", "gram_f32"):
+    for algo in ("twopass", "gram_f32"):
         with pytest.raises(RuntimeError):
             bz().gm2(P, {"maxiter": 5, "guess": g0, "algo": algo})
+    bz().gm2(P, {"maxiter": 5, "guess": g0, "algo": "resident"})
+    assert bz().aggregators.last_result.algo == "resident"
+    X65, g65 = _data(65, 512, seed=1)
+    with pytest.raises(RuntimeError):
+        bz().gm2(bz().ClientPanels.from_rows(X65), {"maxiter": 5, "guess": g65, "algo": "resident"})
     with pytest.raises(RuntimeError):
         bz().gm(P, {"maxiter": 5, "guess": g0, "algo": "gram", "noise_var": 1e-2})
     X2, g2 = _data(300, 512, seed=2)
@@ -237,6 +243,31 @@ def test_single_panels_call_runs_resident(K, d, agg):
         ref = f(P, dict(opts, algo="stream"))
         assert bz().aggregators.last_result.algo == "stream"
         assert rel_l2(got.cpu().numpy(), ref.cpu().numpy()) <= 1e-4
+
+
+RES_PANEL_SHAPES = [(50, 7850, "gm2"), (50, 7850, "gm"), (30, 4098, "gm"), (20, 4098, "gm2"),
+                    (52, 2050, "gm2")]
+
+
+@pytest.mark.parametrize("K,d,agg", RES_PANEL_SHAPES)
+def test_single_panels_resident_matches_rows(K, d, agg):
+    """A single ClientPanels problem whose resident grid fits one XCD runs C2's kernel
+    (resident.hip) on the panels with its rows tile, V = 2 columns per lane inside one
+    panel (api.hip).  At d % 4 == 2 the row-major call runs that same tile (float2 rows), so
+    both read the same columns in the same lanes and agree bit for bit, iterations too."""
+    X, g0 = _data(K, d, seed=K * 11 + d)
+    P = bz().ClientPanels.from_rows(X)
+    opts = {"maxiter": 200, "tol": 1e-5, "guess": g0}
+    if agg == "gm":
+        opts.update(maxiter=100, noise_var=1e-2, seed=3)
+    f = getattr(bz(), agg)
+    a = f(X, dict(opts))
+    ra = bz().aggregators.last_result
+    b = f(P, dict(opts))
+    rb = bz().aggregators.last_result
+    assert ra.algo == "resident" and rb.algo == "resident"
+    assert torch.equal(a, b)
+    assert (ra.iters, ra.converged) == (rb.iters, rb.converged)
 
 
 def iteration_cases():

@@ -408,13 +408,35 @@ r4s2e() {
   # (g1: libgmagg_alt_g1.so, -DGMK_RES_NBCHUNK=32), both (libgmagg_alt.so); parity of the
   # single-problem GPU tests on each, then interleaved A/B
   O=gpurun_out/r4s2e; mkdir -p $O
-  for v in fc g1 ""; do
-    L=byzantine_aircomp_amd/libgmagg_alt${v:+_$v}.so
+  for v in fc g1 both; do
+    L=byzantine_aircomp_amd/libgmagg_alt_$v.so
     GMAGG_LIB=$L timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_weiszfeld.py > $O/t_$v.log 2>&1 || { tail -30 $O/t_$v.log; return 1; }
     echo "$L: $(tail -1 $O/t_$v.log)"
   done
-  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant base= --variant fc=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_fc.so --variant g1=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_g1.so --variant both=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so --out $O/ab_c2.jsonl > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; return 2; }
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant base= --variant fc=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_fc.so --variant g1=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_g1.so --variant both=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_both.so --out $O/ab_c2.jsonl > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; return 2; }
   tail -5 $O/ab_c2.log
+}
+
+r4s2f() {
+  # C5 AirComp: the column noise drawn one Philox block per 4 columns instead of one per
+  # column (timing probe, different draws: libgmagg_alt_nz4.so, ALT_ONLY=resident_batched
+  # ALT_FLAGS=-DGMK_RB_NZ4=1), interleaved A/B without the check
+  O=gpurun_out/r4s2f; mkdir -p $O
+  timeout -k 10 900 python -u tools/ab.py --rounds 2 --bench=--workload,c5,--reading,aircomp,--no-cpu,--alt-steps,0,--soak,0,--no-check,--steps,1,--warmup,0 --variant base= --variant nz4=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_nz4.so --out $O/ab_c5air.jsonl > $O/ab_c5air.log 2>&1 || { tail -20 $O/ab_c5air.log; return 1; }
+  tail -3 $O/ab_c5air.log
+}
+
+r4s2g() {
+  # single ClientPanels problems on C2's resident kernel (one XCD, panels read with the rows
+  # tile): the panels / resident / weiszfeld GPU tests, C2 on panels vs rows, the training
+  # loop (rows and panels)
+  O=gpurun_out/r4s2g; mkdir -p $O
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_panels.py tests/test_gpu_resident_batched.py tests/test_gpu_weiszfeld.py tests/test_gpu_training.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  timeout -k 10 200 python -u bench.py --workload c2 --no-cpu --soak 0 > $O/c2.json 2> $O/c2.err || { tail -20 $O/c2.err; return 2; }
+  python -c "import json;l=json.load(open('$O/c2.json'));print('c2', l['value'], l['ms_per_step'], json.dumps(l.get('alt_layout'))[:300])"
+  timeout -k 10 300 python -u tools/loop_bench.py > $O/loop.jsonl 2> $O/loop.err || { tail -20 $O/loop.err; return 3; }
+  cat $O/loop.jsonl
 }
 
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
