@@ -439,5 +439,15 @@ r4s2g() {
   cat $O/loop.jsonl
 }
 
+r4s2h() {
+  # C2 poll tuning with the L2-kept exchange: no back-off between polls (s0: ALT_ONLY=resident
+  # ALT_FLAGS=-DGMK_RES_SLEEP=0), 8 granules per round trip (c8: -DGMK_RES_NBCHUNK=8), both
+  O=gpurun_out/r4s2h; mkdir -p $O
+  GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_c8s0.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_weiszfeld.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant base= --variant s0=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_s0.so --variant c8=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_c8.so --variant c8s0=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_c8s0.so --out $O/ab_c2.jsonl > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; return 2; }
+  tail -4 $O/ab_c2.log
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
