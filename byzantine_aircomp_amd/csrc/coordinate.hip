@@ -387,11 +387,17 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
         for (int c = 0; c < NC; ++c)
 #pragma unroll
           for (int q = 0; q < NR; ++q) {
+            // the first slot in range: the candidates fill slots [0, nc), the 0xFFFFFFFF
+            // padding after them falls in range when the interval ends at 2^32
             uint32_t v = ans[c][q];
+            bool got = false;
 #pragma unroll
             for (int i = 0; i < R2; ++i) {
               const uint64_t m = __ballot(ck[c][q][i] - ans[c][q] < sp);
-              if (m) v = __builtin_amdgcn_readlane(ck[c][q][i], __builtin_ctzll(m));
+              if (m && !got) {
+                v = __builtin_amdgcn_readlane(ck[c][q][i], __builtin_ctzll(m));
+                got = true;
+              }
             }
             ans[c][q] = v;
           }
@@ -542,6 +548,229 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
   }
 }
 
+// Wave min / max (DPP row shifts + row broadcasts, as wave_sum_i32), wave-uniform.
+template <bool MAX>
+__device__ __forceinline__ float wave_minmax_f32(float v) {
+  const int id = __float_as_int(MAX ? -__builtin_inff() : __builtin_inff());
+  auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : fminf(a, b); };
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(id, __float_as_int(v), 0x111, 0xf, 0xf, false)));
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(id, __float_as_int(v), 0x112, 0xf, 0xf, false)));
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(id, __float_as_int(v), 0x114, 0xf, 0xf, false)));
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(id, __float_as_int(v), 0x118, 0xf, 0xf, false)));
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(id, __float_as_int(v), 0x142, 0xa, 0xf, false)));
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(id, __float_as_int(v), 0x143, 0xc, 0xf, false)));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+template <bool MAX>
+__device__ __forceinline__ uint32_t wave_minmax_u32(uint32_t v) {
+  const int id = MAX ? 0 : -1;
+  auto op = [](uint32_t a, uint32_t b) { return MAX ? (a > b ? a : b) : (a < b ? a : b); };
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x111, 0xf, 0xf, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x112, 0xf, 0xf, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x114, 0xf, 0xf, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x118, 0xf, 0xf, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x142, 0xa, 0xf, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x143, 0xc, 0xf, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// The median of a column pair from a VALUE-linear histogram (round 4 session 2): 256 bins
+// over [min, max] of the column, bin(x) = min(255, trunc((x - min) * 256 / (max - min))) —
+// monotone in x (each step is a correctly rounded monotone operation), so the bins are
+// consecutive intervals of the key order and the counts below a bin are counts below its
+// keys.  Spread data fills many bins (few LDS atomic conflicts, unlike the keys' top byte,
+// whose few exponent bins serialized the adds: the histogram variant above measured slower
+// for the median); the rank's bin holds a few keys, compacted to LDS and finished by the
+// bitwise steps from their common prefix.  Returns false — the caller runs the bitwise
+// selection — on an infinite or subnormal range, or when the rank's bin holds more keys
+// than the compaction takes (e.g. a column dominated by a few huge outliers).  NaN columns
+// never come here.  `rr`: the rank; buf(h, 0): column h's LDS slots (the wave's dead tile
+// column), STR words apart.  MEASURED SLOWER, so off (A/B knob): K=1000 x 2M 4.75 vs
+// 3.85 ms for the counting steps with their compaction (profiles/r4s2_select_vhist_ab.jsonl;
+// the f3 GPU tests green on it) — the min / max reductions, the atomic adds and a second
+// pass over the keys for the compaction cost more than the 8 counting steps they replace.
+#ifndef GMK_SELECT_VHIST
+#define GMK_SELECT_VHIST 0
+#endif
+template <int R, int R2, int STR, typename Buf>
+__device__ __forceinline__ bool median_vhist(const uint32_t (&key)[2][R], int rr, Buf buf,
+                                             uint32_t (&ans)[2]) {
+  const int lane = threadIdx.x & 63;
+  float mn[2], sc[2];
+  bool flat[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float lo = __builtin_inff(), hi = -__builtin_inff();
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const bool v = key[h][i] != 0xFFFFFFFFu;      // (padding rows)
+      const float x = key_value(key[h][i]);
+      lo = v ? fminf(lo, x) : lo;
+      hi = v ? fmaxf(hi, x) : hi;
+    }
+    mn[h] = wave_minmax_f32<false>(lo);
+    const float mx = wave_minmax_f32<true>(hi);
+    flat[h] = !(mx > mn[h]);
+    sc[h] = 256.0f / (mx - mn[h]);
+    if (!flat[h] && !(mx - mn[h] <= 3.0e38f && sc[h] <= 3.0e38f)) return false;
+  }
+  auto bin = [&](int h, uint32_t k) {
+    const int b = (int)((key_value(k) - mn[h]) * sc[h]);
+    return b < 255 ? b : 255;
+  };
+  // histogram: 4 bins per lane, zeroed, one atomic add per held key
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint32_t* hb = buf(h, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hb[(4 * lane + j) * STR] = 0u;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (flat[h]) continue;
+    uint32_t* hb = buf(h, 0);
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      if (key[h][i] != 0xFFFFFFFFu)
+        __hip_atomic_fetch_add(&hb[bin(h, key[h][i]) * STR], 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  int tb[2], blo[2], bhi[2];
+  bool fits = true;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t* hb = buf(h, 0);
+    int c4[4], sl = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      c4[j] = (int)hb[(4 * lane + j) * STR];
+      sl += c4[j];
+    }
+    const int incl = wave_scan_i32(sl), excl = incl - sl;
+    const uint64_t m = __ballot(excl <= rr && rr < incl);
+    const int L = __builtin_amdgcn_readfirstlane(m ? __builtin_ctzll(m) : 0);
+    int lo = __builtin_amdgcn_readlane(excl, L);
+    tb[h] = 4 * L + 3; blo[h] = lo; bhi[h] = lo;
+    bool found = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int hj = __builtin_amdgcn_readlane(c4[j], L);
+      if (!found && lo + hj > rr) {
+        found = true;
+        tb[h] = 4 * L + j;
+        blo[h] = lo;
+        bhi[h] = lo + hj;
+      }
+      lo += hj;
+    }
+    fits = fits && (flat[h] || (m != 0 && bhi[h] - blo[h] <= 64 * R2));
+  }
+  if (!fits) return false;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // the rank's bin -> LDS (lane order) -> R2 candidates per lane
+  uint32_t ck[2][1][R2];
+  int cbase[2][1], clo[2][1], chi[2][1];
+  uint32_t a2[2][1];
+  const int rq[1] = {rr};
+  int hi_bit = -1;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint32_t* b = buf(h, 0);
+    int base = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const bool in = !flat[h] && key[h][i] != 0xFFFFFFFFu && bin(h, key[h][i]) == tb[h];
+      const uint64_t m = __ballot(in);
+      const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (in) b[pos * STR] = key[h][i];
+      base += __popcll(m);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t* b = buf(h, 0);
+    const int nc = flat[h] ? 0 : bhi[h] - blo[h];
+    uint32_t cmn = 0xFFFFFFFFu, cmx = 0u;
+#pragma unroll
+    for (int i = 0; i < R2; ++i) {
+      const int s = lane + 64 * i;
+      ck[h][0][i] = s < nc ? b[s * STR] : 0xFFFFFFFFu;
+      if (s < nc) {
+        cmn = ck[h][0][i] < cmn ? ck[h][0][i] : cmn;
+        cmx = ck[h][0][i] > cmx ? ck[h][0][i] : cmx;
+      }
+    }
+    cmn = wave_minmax_u32<false>(cmn);
+    cmx = wave_minmax_u32<true>(cmx);
+    if (flat[h]) {
+      // every held key is the same value (min == max): the answer, -0 folded onto +0
+      a2[h][0] = order_key(mn[h]);
+      cmn = cmx = a2[h][0];
+    }
+    // the steps start below the candidates' common prefix: keys < that prefix are the
+    // blo below the bin, keys < prefix + 2^(p+1) all the bin's
+    const uint32_t x = cmn ^ cmx;
+    const int p = x ? 31 - __builtin_clz(x) : -1;
+    if (p >= 0) a2[h][0] = cmn & ~((2u << p) - 1u);
+    else a2[h][0] = cmn;
+    hi_bit = p > hi_bit ? p : hi_bit;
+    cbase[h][0] = blo[h];
+    clo[h][0] = blo[h];
+    chi[h][0] = flat[h] ? blo[h] + 1 : bhi[h];
+  }
+  if (hi_bit >= 0) {
+    // both chains step from the higher of their two prefixes (a chain whose prefix is
+    // lower just takes 0 bits until its own; its answer bits above stay its prefix's)
+    const int stop = select_steps<2, 1, true>(hi_bit, 0, a2, clo, chi, rq,
+                         [&](const uint32_t (&t)[2][1], int (&cnt)[2][1]) {
+#pragma unroll
+                           for (int h = 0; h < 2; ++h) {
+                             int n = cbase[h][0];
+#pragma unroll
+                             for (int i = 0; i < R2; ++i) n += __popcll(__ballot(ck[h][0][i] < t[h][0]));
+                             cnt[h][0] = n;
+                           }
+                         });
+    if (stop > 0) {
+      const uint32_t sp = 1u << stop;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint32_t v = a2[h][0];
+        bool got = false;   // (the first slot in range: padding follows the candidates)
+#pragma unroll
+        for (int i = 0; i < R2; ++i) {
+          const uint64_t m = __ballot(ck[h][0][i] - a2[h][0] < sp);
+          if (m && !got) {
+            v = __builtin_amdgcn_readlane(ck[h][0][i], __builtin_ctzll(m));
+            got = true;
+          }
+        }
+        a2[h][0] = v;
+      }
+    }
+  }
+  // (a flat chain's steps ran on no candidates: its answer is its value)
+  ans[0] = flat[0] ? order_key(mn[0]) : a2[0][0];
+  ans[1] = flat[1] ? order_key(mn[1]) : a2[1][0];
+  // (the slots are the caller's again)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return true;
+}
+
 // The order statistics of one column pair whose keys the wave holds (lane l: rows
 // l + 64 i): res[h] = the median (mode 0) or the trimmed mean (mode 1) of column h.
 // buf(h, q): LDS slots for chain (h, q)'s compaction, STR words apart.
@@ -552,7 +781,18 @@ __device__ __forceinline__ void select_pair(const uint32_t (&key)[2][R], const b
   if (mode == 0) {
     const int64_t rk[1] = {(K - 1) / 2};
     uint32_t ans[2][1];
-    select_ranks<R, 2, 1, R2, STR>(key, rk, ans, buf);
+    bool done = false;
+    if constexpr (GMK_SELECT_VHIST && R >= 8 && R2 > 0) {
+      if (!__ballot(nan[0]) && !__ballot(nan[1])) {   // a NaN column's median is NaN
+        uint32_t a2[2];
+        done = median_vhist<R, R2, STR>(key, (int)rk[0], buf, a2);
+        if (done) {
+          ans[0][0] = a2[0];
+          ans[1][0] = a2[1];
+        }
+      }
+    }
+    if (!done) select_ranks<R, 2, 1, R2, STR>(key, rk, ans, buf);
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       res[h] = __ballot(nan[h]) ? __uint_as_float(0x7FC00000u) : key_value(ans[h][0]);

@@ -133,3 +133,30 @@ def test_coordinate_aggregators_on_panels(K, d):
         ia = bz.aggregators.Krum.last_index
         b = bz.Krum(P, {"honestSize": honest})
         assert bz.aggregators.Krum.last_index == ia and torch.equal(a, b)
+
+
+@pytest.mark.parametrize("K,d", [(1000, 300), (513, 130), (300, 77), (1024, 64)])
+def test_median_value_histogram_edge_columns(K, d):
+    """The median's value-linear histogram (coordinate.hip median_vhist, K > 512) and its
+    fall-backs to the bitwise selection: spread columns; a column with a few huge outliers
+    (the rank's bin holds nearly every key: more than the compaction takes); clustered
+    columns; +-inf (an infinite range); a tiny and a subnormal range (the bin scale
+    overflows); an all-equal and a +-0 column; heavy ties.  Every result equals torch's."""
+    import byzantine_aircomp_amd as bz
+    g = torch.Generator().manual_seed(K + 3 * d)
+    X = torch.randn(K, d, generator=g)
+    X[:5, 0] = 1e30
+    X[:, 1] = 0.03 + 1e-3 * torch.randn(K, generator=g)
+    X[0, 2] = float("inf")
+    X[1, 3] = float("-inf")
+    X[:, 4] = 1.0 + torch.arange(K, dtype=torch.float32) * 1e-7
+    X[:, 5] = 1e-40 * torch.randint(0, 3, (K,), generator=g).float()
+    X[:, 6] = 2.5
+    X[:, 7] = 0.0
+    X[::2, 7] = -0.0
+    X[:, 8] = torch.round(X[:, 8] * 2)
+    X[:, 9] = -X[:, 9].abs()
+    X[K // 2:, 10] = 1e4 * X[K // 2:, 10]
+    X[:K // 2 + 5, 11] = float("inf")                  # the median is +inf
+    X[:K // 2 + 5, 12] = 3e38                          # ... a huge finite value
+    assert np.array_equal(bz.median(X.cuda()).cpu().numpy(), orc.median(X).numpy())

@@ -449,5 +449,21 @@ r4s2h() {
   tail -4 $O/ab_c2.log
 }
 
+r4s2i() {
+  # the median from a value-linear histogram (product: GMK_SELECT_VHIST=1) against the
+  # bitwise selection (libgmagg_alt_novh.so: ALT_ONLY=coordinate ALT_FLAGS=-DGMK_SELECT_VHIST=0):
+  # f3 parity on the product, then interleaved timing
+  O=gpurun_out/r4s2i; mkdir -p $O
+  timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_other_aggregators.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  for r in 1 2; do
+    for v in prod novh; do
+      lib=byzantine_aircomp_amd/libgmagg.so; [ $v != prod ] && lib=byzantine_aircomp_amd/libgmagg_alt_$v.so
+      GMAGG_LIB=$lib timeout -k 10 120 python -u tools/select_bench.py --K 1000 256 --reps 3 2> $O/err.log | sed "s/}$/, \"lib\": \"$v\"}/" >> $O/ab.jsonl || return 2
+    done
+  done
+  cat $O/ab.jsonl
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
