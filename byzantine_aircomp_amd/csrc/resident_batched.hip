@@ -41,12 +41,13 @@ constexpr int kRbCols = 2048;                    // columns per block
 #ifndef GMK_RB_COEF_WAVE0
 #define GMK_RB_COEF_WAVE0 0
 #endif
+#ifndef GMK_RB_NZ4
+#define GMK_RB_NZ4 0   // timing probe only (changes the draws; C5 AirComp +3.8 %,
+                       // profiles/r4s2_c5air_noise_keying_ab.jsonl): see draw_pass
+#endif
 // GMK_RB_PREFETCH_ROWS = n > 0: during iteration it of problem p, the rows
 // [n·it, n·it + n) of the group's NEXT problem are read into a junk LDS line (LDS-DMA, no
 // registers), so that the next tile load finds them in the Infinity Cache (A/B)
-#ifndef GMK_RB_NZ4
-#define GMK_RB_NZ4 0   // timing probe only (changes the draws): see draw_pass
-#endif
 #ifndef GMK_RB_PREFETCH_ROWS
 #define GMK_RB_PREFETCH_ROWS 0
 #endif
