@@ -465,5 +465,21 @@ r4s2i() {
   cat $O/ab.jsonl
 }
 
+r4s2z() {
+  # round 4 session 2 closing set: GPU suite + smoke + the default bench line
+  # (tools/final_check.sh), every BASELINE workload's line, C2's kernel trace, the f3 timings
+  bash tools/final_check.sh || return $?
+  O=gpurun_out/r4s2z; mkdir -p $O
+  for w in "c2:--workload c2" "c5:--workload c5" "c5air:--workload c5 --reading aircomp" "c4:--workload c4 --steps 5 --warmup 1" "c4shard:--workload c4-shard"; do
+    n=${w%%:*}; a=${w#*:}
+    timeout -k 10 600 python -u bench.py $a > $O/bench_$n.json 2> $O/bench_$n.err || { tail -20 $O/bench_$n.err; return 2; }
+    cut -c1-300 $O/bench_$n.json
+  done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c2 -o t -- python3 bench.py --workload c2 --no-cpu --alt-steps 0 --soak 0 > $O/trace_c2.log 2>&1 || return 3
+  head -3 $O/trace_c2/t_kernel_stats.csv
+  timeout -k 10 120 python -u tools/select_bench.py --K 1000 256 --reps 3 > $O/select.jsonl 2> $O/select.err || return 4
+  cat $O/select.jsonl
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
