@@ -285,7 +285,7 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
   // wave per cycle slot), so at R >= 8 each lane counts its own keys instead (v_cmp +
   // v_addc: two) and two chains share one DPP wave sum (16-bit halves: <= 2048 each).
   auto full = [&](const uint32_t (&t)[NC][NR], int (&cnt)[NC][NR]) {
-    if constexpr (R >= 8 && (NC * NR) % 2 == 0) {
+    if constexpr (R >= 8) {
       int lc[NC * NR];
 #pragma unroll
       for (int c = 0; c < NC; ++c)
@@ -298,9 +298,13 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
         }
 #pragma unroll
       for (int p = 0; p < NC * NR; p += 2) {
-        const int s2 = wave_sum_i32(lc[p] + (lc[p + 1] << 16));
-        cnt[p / NR][p % NR] = s2 & 0xFFFF;
-        cnt[(p + 1) / NR][(p + 1) % NR] = s2 >> 16;
+        if (p + 1 < NC * NR) {
+          const int s2 = wave_sum_i32(lc[p] + (lc[p + 1] << 16));
+          cnt[p / NR][p % NR] = s2 & 0xFFFF;
+          cnt[(p + 1) / NR][(p + 1) % NR] = s2 >> 16;
+        } else {
+          cnt[p / NR][p % NR] = wave_sum_i32(lc[p]);   // (an odd chain count: NC = NR = 1)
+        }
       }
     } else {
 #pragma unroll
@@ -774,15 +778,16 @@ __device__ __forceinline__ bool median_vhist(const uint32_t (&key)[2][R], int rr
 // The order statistics of one column pair whose keys the wave holds (lane l: rows
 // l + 64 i): res[h] = the median (mode 0) or the trimmed mean (mode 1) of column h.
 // buf(h, q): LDS slots for chain (h, q)'s compaction, STR words apart.
-template <int R, int R2, int STR, typename Buf>
-__device__ __forceinline__ void select_pair(const uint32_t (&key)[2][R], const bool (&nan)[2],
+// NCOL = 1: one column per wave (col_select1).
+template <int R, int R2, int STR, int NCOL = 2, typename Buf>
+__device__ __forceinline__ void select_pair(const uint32_t (&key)[NCOL][R], const bool (&nan)[NCOL],
                                             int64_t K, int mode, int64_t b, Buf buf,
-                                            float (&res)[2]) {
+                                            float (&res)[NCOL]) {
   if (mode == 0) {
     const int64_t rk[1] = {(K - 1) / 2};
-    uint32_t ans[2][1];
+    uint32_t ans[NCOL][1];
     bool done = false;
-    if constexpr (GMK_SELECT_VHIST && R >= 8 && R2 > 0) {
+    if constexpr (NCOL == 2 && GMK_SELECT_VHIST && R >= 8 && R2 > 0) {
       if (!__ballot(nan[0]) && !__ballot(nan[1])) {   // a NaN column's median is NaN
         uint32_t a2[2];
         done = median_vhist<R, R2, STR>(key, (int)rk[0], buf, a2);
@@ -792,17 +797,17 @@ __device__ __forceinline__ void select_pair(const uint32_t (&key)[2][R], const b
         }
       }
     }
-    if (!done) select_ranks<R, 2, 1, R2, STR>(key, rk, ans, buf);
+    if (!done) select_ranks<R, NCOL, 1, R2, STR>(key, rk, ans, buf);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < NCOL; ++h)
       res[h] = __ballot(nan[h]) ? __uint_as_float(0x7FC00000u) : key_value(ans[h][0]);
   } else {
     const int64_t rk[2] = {b, K - b - 1};
-    uint32_t ans[2][2];
-    select_ranks<R, 2, 2, R2, STR>(key, rk, ans, buf);
+    uint32_t ans[NCOL][2];
+    select_ranks<R, NCOL, 2, R2, STR>(key, rk, ans, buf);
     const int64_t n = K - 2 * b;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NCOL; ++h) {
       const uint32_t lo = ans[h][0], hi = ans[h][1];
       const float vlo = key_value(lo), vhi = key_value(hi);
       double sum;
@@ -936,6 +941,76 @@ __global__ void __launch_bounds__(NWV * 64) col_select(const float* __restrict__
     }
   }
 }
+// One column per wave (round 4 session 2; the trimmed mean's kernel, launch_col_select): K <= 1024, a block of
+// C = 16 waves stages a 1024 x 16 tile (69.6 KB, two blocks per CU) and wave w selects
+// column w alone, so that a wave holds 16 keys instead of 32 and the kernel fits 64 VGPRs:
+// 8 waves per SIMD instead of 4, to hide the per-step compare -> count -> decide latency
+// that bounds the pair kernel.  Loads: 4 float4 per thread in flight.
+template <int R, int C>
+__global__ void __launch_bounds__(C * 64, 2) col_select1(const float* __restrict__ X, int64_t K,
+                                                      int64_t d, int64_t ldx, int ws, int mode,
+                                                      int64_t b, int vec4,
+                                                      float* __restrict__ out) {
+  __shared__ float tile[64 * R][C + 1];
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int LPR = C / 4, RPI = C * 64 / LPR;
+  constexpr int NLD = (64 * R + RPI - 1) / RPI;
+  const int tq = threadIdx.x % LPR, tr = threadIdx.x / LPR;
+  const int64_t ntiles = (d + C - 1) / C;
+  const int64_t v = blockIdx.x;
+  if (v >= ntiles) return;
+  // blocks bid and bid + 8 share an XCD: adjacent tiles, one 128-B line's two halves
+  const int64_t t = (v < ntiles / 16 * 16) ? v / 16 * 16 + (v % 8) * 2 + (v / 8) % 2 : v;
+  const int64_t j0 = t * C;
+  {
+    const int64_t col = j0 + 4 * tq;
+    const bool vec = vec4 && col + 4 <= d;
+    f4 buf[NLD];
+#pragma unroll
+    for (int u = 0; u < NLD; ++u) {
+      const int64_t k = tr + (int64_t)u * RPI;
+      buf[u] = f4{0.f, 0.f, 0.f, 0.f};
+      if (k < K) {
+        const float* src = elem(X, ldx, ws, k, col);
+        if (vec) {
+          buf[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) buf[u][e] = col + e < d ? src[e] : 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NLD; ++u) {
+      const int64_t k = tr + (int64_t)u * RPI;
+      if (k < 64 * R) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tile[k][4 * tq + e] = buf[u][e];
+      }
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (j0 + w >= d) return;
+  uint32_t key[1][R];
+  bool nan[1] = {false};
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int row = lane + 64 * i;
+    const bool ok = row < K;
+    const float x = ok ? tile[row][w] : 0.f;
+    key[0][i] = ok ? order_key(x) : 0xFFFFFFFFu;
+    nan[0] |= ok && x != x;
+  }
+  constexpr int R2 = R >= 4 ? 2 : 0;
+  auto bufc = [&](int, int q) {
+    return reinterpret_cast<uint32_t*>(&tile[q * 64 * (R2 > 0 ? R2 : 1)][w]);
+  };
+  float res[1];
+  select_pair<R, R2, C + 1, 1>(key, nan, K, mode, b, bufc, res);
+  if (lane == 0) out[j0 + w] = res[0];
+}
+
 // Krum, step 1: squared distances of every row pair, register-tiled.
 // A block owns a 128 x 128 tile of pairs (row tiles bi <= bj: D is symmetric)
 // over one slice of the columns; each of 512 threads an 8 x 4 sub-tile (8 x 8 with
@@ -1168,10 +1243,24 @@ hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, 
   // 64 scattered 4-byte loads per wave instruction; profiles/r4s1_select_direct_ab.jsonl)
   // K <= 1024: 8 waves per 69.6-KB tile (one column pair each) so that the CU holds
   // 4 waves per SIMD (the LDS allows 2 tiles) instead of 2
+  // one column per wave (col_select1) for the trimmed mean at 512 < K <= 1024: 6.29 ->
+  // 5.90 ms at K=1000 x 2M; the median measured slower on it (3.87 -> 4.23 ms: its single
+  // chain loses the paired wave sums and half the independent steps per wave), so the median
+  // keeps the column-pair kernel (profiles/r4s2_select_1col_ab.jsonl).  GMAGG_SELECT_1COL:
+  // 1 both, 0 neither (A/B)
+  static const int one_col_env = [] {
+    const char* e = getenv("GMAGG_SELECT_1COL");
+    return e ? atoi(e) : -1;
+  }();
+  const bool one_col = one_col_env < 0 ? mode == 1 : one_col_env != 0;
   if (K <= 64) GMK_SEL(1, 32, 4);
   else if (K <= 128) GMK_SEL(2, 32, 4);
   else if (K <= 256) GMK_SEL(4, 32, 4);
   else if (K <= 512) GMK_SEL(8, 16, 4);
+  else if (K <= 1024 && one_col) {
+    hipLaunchKernelGGL((col_select1<16, 16>), dim3((unsigned)((d + 15) / 16)), dim3(1024), 0, s, X,
+                       K, d, ldx, ws, mode, b, vec4, out);
+  }
   else if (K <= 1024) GMK_SEL(16, 16, 8);
   else if (K <= 2048) GMK_SEL(32, 8, 4);
   else return hipErrorInvalidValue;
