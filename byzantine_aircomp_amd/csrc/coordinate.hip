@@ -1247,7 +1247,7 @@ hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, 
   // 5.90 ms at K=1000 x 2M; the median measured slower on it (3.87 -> 4.23 ms: its single
   // chain loses the paired wave sums and half the independent steps per wave), so the median
   // keeps the column-pair kernel (profiles/r4s2_select_1col_ab.jsonl).  GMAGG_SELECT_1COL:
-  // 1 both, 0 neither (A/B)
+  // 1 both, 0 neither (A/B); at K <= 256 see below
   static const int one_col_env = [] {
     const char* e = getenv("GMAGG_SELECT_1COL");
     return e ? atoi(e) : -1;
@@ -1255,6 +1255,13 @@ hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, 
   const bool one_col = one_col_env < 0 ? mode == 1 : one_col_env != 0;
   if (K <= 64) GMK_SEL(1, 32, 4);
   else if (K <= 128) GMK_SEL(2, 32, 4);
+  // at 128 < K <= 256 the other way round: the median gains on one column per wave (1.34 ->
+  // 1.26 ms at K=256 x 2M), the trimmed mean loses (2.24 -> 2.36); GMAGG_SELECT_1COL=2
+  // puts both there (profiles/r4s2_select_1col_k256_ab.jsonl)
+  else if (K <= 256 && (one_col_env < 0 ? mode == 0 : one_col_env == 2)) {
+    hipLaunchKernelGGL((col_select1<4, 16>), dim3((unsigned)((d + 15) / 16)), dim3(1024), 0, s, X,
+                       K, d, ldx, ws, mode, b, vec4, out);
+  }
   else if (K <= 256) GMK_SEL(4, 32, 4);
   else if (K <= 512) GMK_SEL(8, 16, 4);
   else if (K <= 1024 && one_col) {

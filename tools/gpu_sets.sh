@@ -495,5 +495,19 @@ r4s2j() {
   cat $O/ab.jsonl
 }
 
+r4s2k() {
+  # f3 at K <= 256 with one column per wave (GMAGG_SELECT_1COL=2) against the column-pair
+  # kernel: parity, then interleaved timing
+  O=gpurun_out/r4s2k; mkdir -p $O
+  GMAGG_SELECT_1COL=2 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_other_aggregators.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  for r in 1 2; do
+    for v in -1 2; do
+      GMAGG_SELECT_1COL=$v timeout -k 10 120 python -u tools/select_bench.py --K 256 --reps 3 2> $O/err.log | sed "s/}$/, \"one_col\": $v}/" >> $O/ab.jsonl || return 2
+    done
+  done
+  cat $O/ab.jsonl
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
