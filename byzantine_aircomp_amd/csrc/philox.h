@@ -115,21 +115,19 @@ __device__ __forceinline__ float oma_noisy(float x, float scale, float z) {
   return x + scale * z;
 }
 
-// One standard normal for element `idx` (uses half of a Philox block): the AirComp
-// column noise, drawn by the pass's finisher threads between two block barriers, on
-// the hardware Box-Muller.  Device-only: every call site that regenerates a draw
-// runs this same code, so a draw is identical wherever it is made.
+// One standard normal for element `idx`: normal idx & 3 of the Philox block (iter, idx >> 2)
+// on the hardware Box-Muller — four consecutive elements share a block, as in the fill and
+// OMA draws (round 4 session 2; before, one block per element, normal 0: the batched
+// resident kernel's four columns per thread then took four blocks per iteration; C5 AirComp
+// 773.8 -> 803.6 problems/s, profiles/r4s2_c5air_draws_ab.jsonl).  The AirComp column noise
+// and the denominator's draw (element d_total).  Device-only: every call site that
+// regenerates a draw runs this same code, so a draw is identical wherever it is made.
 __device__ __forceinline__ float normal1(uint64_t seed, uint32_t stream, uint64_t iter,
                                          uint64_t idx) {
-  u4 c{(uint32_t)idx, (uint32_t)(idx >> 32), (uint32_t)iter, stream ^ (uint32_t)(iter >> 32)};
-  u4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-  float n0, n1;
-#ifndef GMK_NORMAL1_PRECISE   // A/B knob: libm-style Box-Muller on the device
-  box_muller_hw(r.x, r.y, &n0, &n1);
-#else
-  box_muller(r.x, r.y, &n0, &n1);
-#endif
-  return n0;
+  float z[4];
+  normal4_hw(seed, stream, iter, idx >> 2, z);
+  const unsigned e = (unsigned)(idx & 3u);
+  return e == 0 ? z[0] : e == 1 ? z[1] : e == 2 ? z[2] : z[3];
 }
 
 }  // namespace gmk

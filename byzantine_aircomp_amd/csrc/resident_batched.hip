@@ -41,15 +41,18 @@ constexpr int kRbCols = 2048;                    // columns per block
 #ifndef GMK_RB_COEF_WAVE0
 #define GMK_RB_COEF_WAVE0 0
 #endif
-#ifndef GMK_RB_NZ4
-#define GMK_RB_NZ4 0   // timing probe only (changes the draws; C5 AirComp +3.8 %,
-                       // profiles/r4s2_c5air_noise_keying_ab.jsonl): see draw_pass
-#endif
 // GMK_RB_PREFETCH_ROWS = n > 0: during iteration it of problem p, the rows
 // [n·it, n·it + n) of the group's NEXT problem are read into a junk LDS line (LDS-DMA, no
 // registers), so that the next tile load finds them in the Infinity Cache (A/B)
 #ifndef GMK_RB_PREFETCH_ROWS
 #define GMK_RB_PREFETCH_ROWS 0
+#endif
+// GMK_RB_EARLY_H2=1: the AirComp channel gains |h_k|^2 drawn in draw_pass, after the
+// previous publish, instead of inside the coefficient step on the iteration's dependent
+// chain: with the four-column noise blocks (philox.h normal1) C5 AirComp 803.6 -> 816.7
+// problems/s (profiles/r4s2_c5air_draws_ab.jsonl); 0 = in the coefficient step (A/B)
+#ifndef GMK_RB_EARLY_H2
+#define GMK_RB_EARLY_H2 1
 #endif
 #ifndef GMK_RB_OMA_ROWS
 #define GMK_RB_OMA_ROWS 2
@@ -95,9 +98,6 @@ __device__ __forceinline__ bool rb_gather(const gu64* g, int64_t bstride, int fi
         }
       }
       if (ok) break;
-#ifndef GMK_RB_EARLY_H2
-#define GMK_RB_EARLY_H2 0
-#endif
 #ifndef GMK_RB_NOSLEEP
       __builtin_amdgcn_s_sleep(GMK_RB_SLEEP);
 #endif
@@ -428,8 +428,8 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
     // AirComp: pass `it`'s draws depend on (problem, it, column / client) only, so each
     // pass's are drawn right after the previous publish, while the other blocks' partials
     // are in flight (off the gather -> phase A -> phase B chain): the column noise (M:411,
-    // one Philox block per column, one at a time: four interleaved chains beside the tile
-    // spill), lane k's channel gain |h_k|^2 (M:403) and the scalar noise of M:153-155
+    // the thread's four columns: one Philox block), lane k's channel gain |h_k|^2 (M:403)
+    // and the scalar noise of M:153-155
     float nz[4] = {0.f, 0.f, 0.f, 0.f};
     float h2k = 1.f, ndr = 0.f;
     auto draw_pass = [&](int64_t i) {
@@ -441,20 +441,9 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
           h2k = hr * hr + hi * hi;
         }
         if (a.has_noise) {
-#if GMK_RB_NZ4
-          // (timing probe: one Philox block per 4 columns, element j = normal j & 3 of
-          // block j >> 2; NOT the keying of the other paths)
-          float zd[4];
-          normal4_hw(seed_p, kStreamNoise, (uint64_t)i, (uint64_t)d >> 2, zd);
-          ndr = zd[d & 3];
-          normal4_hw(seed_p, kStreamNoise, (uint64_t)i, (uint64_t)col0 >> 2, nz);
-#else
+          // the thread's 4 columns (col0 % 4 == 0) are one Philox block (philox.h normal1)
           ndr = normal1(seed_p, kStreamNoise, (uint64_t)i, (uint64_t)d);
-          sfor<0, 4>([&](auto v) {
-            nz[v] = normal1(seed_p, kStreamNoise, (uint64_t)i, (uint64_t)(col0 + v));
-            __builtin_amdgcn_sched_barrier(0);
-          });
-#endif
+          normal4_hw(seed_p, kStreamNoise, (uint64_t)i, (uint64_t)col0 >> 2, nz);
         }
       }
     };

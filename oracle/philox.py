@@ -146,8 +146,8 @@ def gm_draws(seed: int, d_total: int, col_off: int = 0):
     Philox AirComp draws in the reference's per-iteration order (OMA2 M:401-402,
     M:411: channel real [K], channel imag [K], noise [d+1]).  Iteration it's client
     k takes normals 0 / 1 of block (it, k) on the channel stream (weiszfeld.hip
-    kspace_step); column j's noise is normal 0 of block (it, global j) on the noise
-    stream, the denominator's entry is global index d_total (stream_pass.hip)."""
+    kspace_step); global column j's noise is normal j & 3 of block (it, j >> 2) on the
+    noise stream, the denominator's entry is global index d_total (philox.h normal1)."""
     import torch
     state = {"it": 0, "call": 0, "h": None}
 
@@ -163,7 +163,8 @@ def gm_draws(seed: int, d_total: int, col_off: int = 0):
             L = shape[0]                                  # d + 1
             idx = np.concatenate([col_off + np.arange(L - 1, dtype=np.uint64),
                                   np.array([d_total], dtype=np.uint64)])
-            v = normal4(seed, STREAM_NOISE, np.uint64(it), idx)[:, 0]
+            z = normal4(seed, STREAM_NOISE, np.uint64(it), idx >> np.uint64(2))     # [L, 4]
+            v = np.take_along_axis(z, (idx & np.uint64(3)).astype(np.int64)[:, None], axis=1)[:, 0]
         state["call"] = call + 1
         if call == 2 or (call == 1 and state.get("no_noise")):
             state["it"], state["call"] = it + 1, 0

@@ -509,5 +509,14 @@ r4s2k() {
   cat $O/ab.jsonl
 }
 
+r4s2l() {
+  # C5 AirComp draw placement (timing only, no check): the channel draw in draw_pass off
+  # the critical path (eh: ALT_ONLY=resident_batched ALT_FLAGS=-DGMK_RB_EARLY_H2=1), one
+  # Philox block per 4 columns (nz: -DGMK_RB_NZ4=1, different draws), both (ehnz)
+  O=gpurun_out/r4s2l; mkdir -p $O
+  timeout -k 10 1100 python -u tools/ab.py --rounds 2 --bench=--workload,c5,--reading,aircomp,--no-cpu,--alt-steps,0,--soak,0,--no-check,--steps,1,--warmup,0 --variant base= --variant eh=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_eh.so --variant nz=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_nz.so --variant ehnz=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_ehnz.so --out $O/ab.jsonl > $O/ab.log 2>&1 || { tail -20 $O/ab.log; return 1; }
+  tail -4 $O/ab.log
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
