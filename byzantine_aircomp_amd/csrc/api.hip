@@ -116,6 +116,25 @@ unsigned res_xcd_stride(int nb, int num_cu) {
 }
 // GMAGG_RB_XCD: 0 round-robin numbering, 1 XCD-major (default), 2 XCD-major with whole
 // groups per XCD whose granules stay in the XCD's L2 (resident_batched.hip rb_put)
+// The single-problem resident kernel's tile (round 4 session 2): at 32 < K <= 64, 8 waves
+// of 8 rows per lane (512-thread blocks) instead of the streaming tile's 16 waves of 4 —
+// half the waves in every cross-wave reduction and block barrier of the iteration, the
+// same 256 columns per block: C2 238.0 -> 281.2 aggregations/s (profiles/r4s2_c2_tile_ab.jsonl).
+// GMAGG_RES_CFG="NW,R" forces a tile (LPR 64; NW * R >= K), e.g. "16,4" the previous one.
+void resident_tile(PassCfg* cfg, int64_t K) {
+  if (cfg->LPR != 64) return;
+  int nw = 0, r = 0;
+  if (const char* e = getenv("GMAGG_RES_CFG")) {
+    if (sscanf(e, "%d,%d", &nw, &r) != 2 || (int64_t)nw * r < K) nw = 0;
+  } else if (K > 32 && K <= 64 && cfg->NW == 16 && cfg->R == 4) {
+    nw = 8;
+    r = 8;
+  }
+  if (nw > 0) {
+    cfg->NW = nw;
+    cfg->R = r;
+  }
+}
 int rb_xcd_major() {
   const char* e = getenv("GMAGG_RB_XCD");
   return e ? atoi(e) : 1;                 // 1 by default (round 4 A/B)
@@ -840,7 +859,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       int cpb = 0, nbr = 0;
       int ws = 0;
       while (((int64_t)1 << ws) < W) ++ws;
-      if (pick_cfg(K, 2, W, &rcfg) && W % rcfg.V == 0 &&
+      if (pick_cfg(K, 2, W, &rcfg) && W % rcfg.V == 0 && (resident_tile(&rcfg, K), true) &&
           resident_plan(rcfg, (d + rcfg.LPR * rcfg.V - 1) / (rcfg.LPR * rcfg.V), c->num_cu, &cpb,
                         &nbr) &&
           res_xcd_stride(nbr, c->num_cu) == 8) {
@@ -896,6 +915,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   const bool host_noise_req = o->mode == GM_MODE_AIRCOMP && o->noise_source == GM_NOISE_HOST;
   if ((algo == GM_ALGO_AUTO || algo == GM_ALGO_RESIDENT) && !host_noise_req &&
       c->d_total <= 0 && !c->comm && !c->ar_fn && pick_cfg(K, V, ldx, &cfg)) {
+    resident_tile(&cfg, K);
     const int J = cfg.LPR * cfg.V;
     const int64_t nch = (d + J - 1) / J;
     int cpb = 0, nbr = 0;

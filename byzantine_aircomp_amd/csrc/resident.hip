@@ -624,7 +624,9 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
 #define GMK_RES_TILE_REGS 16   // A/B knob: 32 allows 16 blocks at C2 (with spills)
 #endif
 constexpr bool res_cpb_ok(int V, int NW, int LPR, int R, int CPB) {
-  return CPB == 1 || (CPB * LPR * V <= NW * 64 && CPB * R * V <= GMK_RES_TILE_REGS);
+  // (512-thread blocks have 256 VGPRs per lane: a 64-register tile fits)
+  return CPB == 1 || (CPB * LPR * V <= NW * 64 &&
+                      CPB * R * V <= (NW >= 16 ? GMK_RES_TILE_REGS : 64));
 }
 
 template <int V, int NW, int LPR, int R, int CPB>
@@ -648,7 +650,8 @@ static const void* resident_kernel(const PassCfg& cfg, int cpb) {
   }
 #define GMK_RES_V(V_)                                                                         \
   GMK_RES(V_, 16, 64, 1) GMK_RES(V_, 16, 64, 2) GMK_RES(V_, 16, 64, 4) GMK_RES(V_, 16, 64, 8)   \
-  GMK_RES(V_, 16, 32, 8) GMK_RES(V_, 16, 16, 8) GMK_RES(V_, 16, 8, 8) GMK_RES(V_, 16, 4, 8)
+  GMK_RES(V_, 16, 32, 8) GMK_RES(V_, 16, 16, 8) GMK_RES(V_, 16, 8, 8) GMK_RES(V_, 16, 4, 8)    \
+  GMK_RES(V_, 8, 64, 8)
   GMK_RES_V(4)
   GMK_RES_V(2)
   GMK_RES_V(1)
@@ -657,10 +660,10 @@ static const void* resident_kernel(const PassCfg& cfg, int cpb) {
   return nullptr;
 }
 
-// Blocks of CPB chunks each: the fewest blocks (largest valid CPB) up to 8 chunks
-// per block while more than kResTargetBlocks blocks remain; GMAGG_RES_CPB=n forces
+// Blocks of CPB chunks each: the smallest CPB (up to 8) that brings the grid to at most
+// kResTargetBlocks blocks, or the largest valid one; GMAGG_RES_CPB=n forces
 // n (A/B).  Returns false when the grid cannot be co-resident.
-constexpr int kResTargetBlocks = 16;
+constexpr int kResTargetBlocks = 32;   // one XCD's CUs (the L2-kept exchange, api.hip)
 
 bool resident_plan(const PassCfg& cfg, int64_t nch, int num_cu, int* cpb_out, int* nb_out) {
   int cpb = 0;

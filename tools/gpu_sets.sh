@@ -518,5 +518,35 @@ r4s2l() {
   tail -4 $O/ab.log
 }
 
+r4s2n() {
+  # C2's resident tile: 16 waves x 4 rows (default) against 8 waves x 8 rows per lane
+  # (GMAGG_RES_CFG=8,8: 512-thread blocks, half the waves in each reduction and barrier),
+  # with 4 chunks per block (16 blocks, auto) or 2 (31 blocks); parity of the single-problem
+  # tests on the 8-wave tile first
+  O=gpurun_out/r4s2n; mkdir -p $O
+  GMAGG_RES_CFG=8,8 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_weiszfeld.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant base= --variant w8=GMAGG_RES_CFG=8,8 --variant "w8c2=GMAGG_RES_CFG=8,8;GMAGG_RES_CPB=2" --out $O/ab_c2.jsonl > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; return 2; }
+  tail -3 $O/ab_c2.log
+}
+
+r4s2o() {
+  # after C2's 8-wave resident tile became the default: the GPU suite + smoke + default bench,
+  # C2's exchange floor on the new tile (libgmagg_alt.so: ALT_ONLY=resident
+  # ALT_FLAGS=-DGMK_RES_DBG=7) and the product at tol -1, C2's bench line and kernel trace
+  bash tools/final_check.sh || return $?
+  O=gpurun_out/r4s2o; mkdir -p $O
+  B="--no-cpu --no-check --alt-steps 0 --soak 0"
+  GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so timeout -k 10 200 python -u bench.py --workload c2 --tol -1 --steps 5 $B > $O/c2_exchange_only.json 2> $O/c2x.err || return 2
+  timeout -k 10 200 python -u bench.py --workload c2 --tol -1 --steps 5 $B > $O/c2_tolneg.json 2> $O/c2.err || return 3
+  for f in $O/c2_exchange_only.json $O/c2_tolneg.json; do echo "$f $(python -c "import json;print(json.load(open('$f'))['ms_per_step'])")"; done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c2 -o t -- python3 bench.py --workload c2 --no-cpu --alt-steps 0 --soak 0 > $O/trace_c2.log 2>&1 || return 4
+  head -3 $O/trace_c2/t_kernel_stats.csv
+  timeout -k 10 200 python -u bench.py --workload c2 > $O/bench_c2.json 2> $O/bench_c2.err || return 5
+  cut -c1-300 $O/bench_c2.json
+  timeout -k 10 300 python -u tools/loop_bench.py > $O/loop.jsonl 2> $O/loop.err || return 6
+  head -2 $O/loop.jsonl | cut -c1-300
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
