@@ -651,7 +651,7 @@ static const void* resident_kernel(const PassCfg& cfg, int cpb) {
 #define GMK_RES_V(V_)                                                                         \
   GMK_RES(V_, 16, 64, 1) GMK_RES(V_, 16, 64, 2) GMK_RES(V_, 16, 64, 4) GMK_RES(V_, 16, 64, 8)   \
   GMK_RES(V_, 16, 32, 8) GMK_RES(V_, 16, 16, 8) GMK_RES(V_, 16, 8, 8) GMK_RES(V_, 16, 4, 8)    \
-  GMK_RES(V_, 8, 64, 8)
+  GMK_RES(V_, 8, 64, 8) GMK_RES(V_, 4, 64, 16)
   GMK_RES_V(4)
   GMK_RES_V(2)
   GMK_RES_V(1)

@@ -548,5 +548,15 @@ r4s2o() {
   head -2 $O/loop.jsonl | cut -c1-300
 }
 
+r4s2p() {
+  # C2's resident tile, one step further: 4 waves of 16 rows (GMAGG_RES_CFG=4,16: 256-thread
+  # blocks, one wave per SIMD) against the default 8 waves of 8; parity first
+  O=gpurun_out/r4s2p; mkdir -p $O
+  GMAGG_RES_CFG=4,16 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_weiszfeld.py tests/test_gpu_panels.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant base= --variant w4=GMAGG_RES_CFG=4,16 --out $O/ab_c2.jsonl > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; return 2; }
+  tail -2 $O/ab_c2.log
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
