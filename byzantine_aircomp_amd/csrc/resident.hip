@@ -101,6 +101,9 @@ __device__ __forceinline__ void put_value(gu64* g, unsigned tag, float v, bool l
 #endif
 // Granules per poll round trip.  32 (>= C2's 31 blocks: one round trip, one stage, G = 1)
 // spilled 336 bytes and measured 4x slower (55.9 aggregations/s, same A/B)
+#ifndef GMK_RES_FUSE_COEF
+#define GMK_RES_FUSE_COEF 0   // A/B knob: see the gather (one block barrier fewer per iteration)
+#endif
 #ifndef GMK_RES_NBCHUNK
 #define GMK_RES_NBCHUNK 4
 #endif
@@ -335,6 +338,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   uint64_t prev_ = __builtin_amdgcn_s_memrealtime();
 #endif
   bool pre_h2 = false;
+  bool fused = false;
   for (;; ++it) {
     // (1) gather pass `it` (INIT at it = 0): D2 (+ r at it = 0) and the per-wave
     // movement / norm partials.  G thread groups each sum every G-th block (in
@@ -399,16 +403,34 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
           store_value(cc, sum);
         }
       }
-      __syncthreads();   // (s_wp is read in place: its next write follows this iteration's barriers)
+      // GMK_RES_FUSE_COEF: when wave 0 alone summed the values (K <= 64, ncol <= 64) it also
+      // forms the coefficients, so the block barrier between the two goes: a wave-scope
+      // fence orders its lanes' LDS writes before their cross-lane reads, and the tol test
+      // moves behind the coefficient step's barrier (the coefficients of a converged or
+      // final pass are formed and not used)
+      fused = GMK_RES_FUSE_COEF && K <= 64 && ncol <= 64 && G > 1 && it >= 1;
+      if (fused) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else {
+        __syncthreads();   // (s_wp is read in place: its next write follows this iteration's barriers)
+      }
     }
     RES_T(0)
     // (2) tol test of the pass that produced g_it (M:180-183)
-    if (it >= 1) {
-      const float mv = (float)sqrt(s_wp[0]);
-      last_mv = (double)mv;
-      if (mv <= a.tol) { conv = 1; break; }
-    }
-    if (it == a.maxiter) break;
+    auto tol_test = [&]() {
+      if (it >= 1) {
+        const float mv = (float)sqrt(s_wp[0]);
+        last_mv = (double)mv;
+        if (mv <= a.tol) {
+          conv = 1;
+          return true;
+        }
+      }
+      return it == a.maxiter;
+    };
+    if (!fused && tol_test()) break;
 
     // (3) coefficients for pass `it`: one wave, lane = client, when K <= 64
     if constexpr ((GMK_RES_DBG & 2) != 0) {
@@ -521,6 +543,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
       if (tid == 0) s_anoise = a.has_noise ? (float)(scale * a.noise_sd) : 0.f;
     }
     __syncthreads();
+    if (fused && tol_test()) break;
     RES_T(1)
 
     // (4) phase A on the resident tiles

@@ -558,5 +558,16 @@ r4s2p() {
   tail -2 $O/ab_c2.log
 }
 
+r4s2q() {
+  # C2: wave 0 forms the coefficients right after summing the gathered values, one block
+  # barrier fewer per iteration (libgmagg_alt_fuse.so: ALT_ONLY=resident
+  # ALT_FLAGS=-DGMK_RES_FUSE_COEF=1); parity first
+  O=gpurun_out/r4s2q; mkdir -p $O
+  GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_fuse.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_weiszfeld.py tests/test_gpu_panels.py tests/test_gpu_training.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant base= --variant fuse=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_fuse.so --out $O/ab_c2.jsonl > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; return 2; }
+  tail -2 $O/ab_c2.log
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
