@@ -56,12 +56,28 @@ __device__ __forceinline__ void put_param(const ClientChainArgs& a, int64_t k, i
     a.X[k * a.ldx + jj] = v;
 }
 
-// NJ = features per lane in phase A (F <= 64 * NJ)
+// fp32 max / sum over the wave, every lane the result (gfx950 permlane swaps + DPP, no LDS
+// round trips; device_util.h xlane_wave_sum_f32's pairings)
+__device__ __forceinline__ float cc_wave_max(float v) {
+  auto sw = [&](auto r) { v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1])); };
+  sw(__builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false));
+  sw(__builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false));
+  v = fmaxf(v, xlane_partner<8>(v));
+  v = fmaxf(v, xlane_partner<4>(v));
+  v = fmaxf(v, xlane_partner<2>(v));
+  v = fmaxf(v, xlane_partner<1>(v));
+  return v;
+}
+
+// NJ = features per lane in phase A (F <= 64 * NJ).  Dynamic LDS: the client's batch tile
+// x[B][F] (phase A stages it, phase C reads it instead of re-reading the rows from L2 per
+// sample), when B * F * 4 bytes fit (a.stage); else phase C reads global memory.
 template <int NJ>
 __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a) {
   __shared__ float s_z[kCcMaxB][kCcMaxC + 1];     // logits, then the gradient dz (padding 0)
   __shared__ int s_row[kCcMaxB];                  // dataset rows of the client's batch
   __shared__ int s_lab[kCcMaxB];                  // (relabelled) targets
+  extern __shared__ float s_x[];                  // [B][F] when a.stage
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -93,6 +109,17 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
         xr[i][j] = v;
       }
     }
+    if (a.stage) {
+#pragma unroll
+      for (int i = 0; i < kCcSpw; ++i) {
+        const int s = w + kCcWaves * i;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int f = lane + 64 * j;
+          if (s < B && f < F) s_x[s * F + f] = xr[i][j];
+        }
+      }
+    }
     for (int c0 = 0; c0 < C; c0 += kCcCg) {
       float e[kCcSpw * kCcCg];                            // value i * CG + cc
 #pragma unroll
@@ -109,7 +136,7 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
           for (int i = 0; i < kCcSpw; ++i) e[i * kCcCg + cc] = fmaf(xr[i][j], wv, e[i * kCcCg + cc]);
         }
       }
-      transpose_reduce<64, kCcSpw * kCcCg>(e, lane);
+      xlane_transpose64<kCcSpw * kCcCg>(e, lane);   // (transpose_reduce's lane -> value map)
       // lanes 2v and 2v + 1 hold value row_of_lane(lane) (32 values over 64 lanes)
       if ((lane & 1) == 0) {
         const int v = row_of_lane<64, kCcSpw * kCcCg>(lane);
@@ -124,12 +151,8 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
     for (int s = w; s < B; s += kCcWaves) {
       const bool cv = lane < C;
       const float z = cv ? s_z[s][lane] : -INFINITY;
-      float m = z;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-      float sum = cv ? expf(z - m) : 0.f;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+      const float m = cc_wave_max(z);
+      const float sum = xlane_wave_sum_f32(cv ? expf(z - m) : 0.f);
       const float logp = (z - m) - logf(sum);
       const float gout = (lane == s_lab[s]) ? -invB : 0.f;
       if (cv) s_z[s][lane] = gout - expf(logp) * (-invB);
@@ -146,13 +169,21 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
         for (int cc = 0; cc < kCcCgC; ++cc) g[h][cc] = 0.f;
 #pragma unroll 2
       for (int s = 0; s < B; ++s) {
-        const float* row = a.data + (int64_t)s_row[s] * a.ldd;
         float xv[kCcFpt];
+        if (a.stage) {
 #pragma unroll
-        for (int h = 0; h < kCcFpt; ++h) {
-          const int f = tid + kCcThreads * h;
-          xv[h] = f < F ? row[f] : 0.f;
-          if (flip_x) xv[h] = 1.0f - xv[h];
+          for (int h = 0; h < kCcFpt; ++h) {
+            const int f = tid + kCcThreads * h;
+            xv[h] = f < F ? s_x[s * F + f] : 0.f;             // (flipped when staged)
+          }
+        } else {
+          const float* row = a.data + (int64_t)s_row[s] * a.ldd;
+#pragma unroll
+          for (int h = 0; h < kCcFpt; ++h) {
+            const int f = tid + kCcThreads * h;
+            xv[h] = f < F ? row[f] : 0.f;
+            if (flip_x) xv[h] = 1.0f - xv[h];
+          }
         }
 #pragma unroll
         for (int cc = 0; cc < kCcCgC; ++cc) {
@@ -200,7 +231,17 @@ bool client_chain_supported(int64_t F, int64_t C, int64_t B) {
 hipError_t launch_client_chain(const ClientChainArgs& a, hipStream_t s) {
   // 13 features per lane: F <= 832 covers the reference's 28 x 28 inputs (MNIST and
   // EMNIST, F = 784) without idle iterations; 16 per lane spilled 164 VGPRs
-  hipLaunchKernelGGL(client_chain<kCcNj>, dim3(1), dim3(kCcThreads), 0, s, a);
+  // the batch tile in LDS beside the 17 KB of s_z: up to 128 KB (B = 32 at F = 784: 98 KB)
+  ClientChainArgs b = a;
+  const size_t tile = (size_t)a.B * (size_t)a.F * sizeof(float);
+  b.stage = tile <= (128u << 10) ? 1 : 0;
+  const void* fn = reinterpret_cast<const void*>(&client_chain<kCcNj>);
+  if (b.stage) {
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)tile);
+    if (e != hipSuccess) b.stage = 0;
+  }
+  hipLaunchKernelGGL(client_chain<kCcNj>, dim3(1), dim3(kCcThreads), b.stage ? tile : 0, s, b);
   return hipGetLastError();
 }
 

@@ -242,6 +242,7 @@ struct ClientChainArgs {
   int64_t ldx;            // rows: row stride
   int64_t pstride;        // > 0: panels, elements between panels (panel width 1 << wshift)
   int wshift;
+  int stage;              // (set by launch_client_chain) the batch tile staged in LDS
 };
 bool client_chain_supported(int64_t F, int64_t C, int64_t B);
 hipError_t launch_client_chain(const ClientChainArgs& a, hipStream_t s);
