@@ -232,15 +232,13 @@ hipError_t launch_client_chain(const ClientChainArgs& a, hipStream_t s) {
   // 13 features per lane: F <= 832 covers the reference's 28 x 28 inputs (MNIST and
   // EMNIST, F = 784) without idle iterations; 16 per lane spilled 164 VGPRs
   // the batch tile in LDS beside the 17 KB of s_z: up to 128 KB (B = 32 at F = 784: 98 KB)
+  constexpr size_t kStageMax = 128u << 10;
+  static const bool stage_ok =   // the kernel's dynamic-LDS limit raised once per process
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&client_chain<kCcNj>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageMax) == hipSuccess;
   ClientChainArgs b = a;
   const size_t tile = (size_t)a.B * (size_t)a.F * sizeof(float);
-  b.stage = tile <= (128u << 10) ? 1 : 0;
-  const void* fn = reinterpret_cast<const void*>(&client_chain<kCcNj>);
-  if (b.stage) {
-    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)tile);
-    if (e != hipSuccess) b.stage = 0;
-  }
+  b.stage = stage_ok && tile <= kStageMax ? 1 : 0;
   hipLaunchKernelGGL(client_chain<kCcNj>, dim3(1), dim3(kCcThreads), b.stage ? tile : 0, s, b);
   return hipGetLastError();
 }
