@@ -44,7 +44,7 @@ constexpr int kCcSpw = 8;        // samples per wave in phase A (B <= 64)
 constexpr int kCcCg = 4;         // classes per phase-A group
 constexpr int kCcFpt = 2;        // features per thread in phase C
 constexpr int kCcNj = 13;        // features per lane in phase A: F <= 832
-constexpr int kCcCgC = 16;       // classes per phase-C group
+constexpr int kCcCgC = 16;       // classes per phase-C group (CGC: 10 when C <= 10)
 constexpr int kCcMaxC = 64;
 constexpr int kCcMaxB = kCcWaves * kCcSpw;
 
@@ -72,7 +72,7 @@ __device__ __forceinline__ float cc_wave_max(float v) {
 // NJ = features per lane in phase A (F <= 64 * NJ).  Dynamic LDS: the client's batch tile
 // x[B][F] (phase A stages it, phase C reads it instead of re-reading the rows from L2 per
 // sample), when B * F * 4 bytes fit (a.stage); else phase C reads global memory.
-template <int NJ>
+template <int NJ, int CGC>
 __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a) {
   __shared__ float s_z[kCcMaxB][kCcMaxC + 1];     // logits, then the gradient dz (padding 0)
   __shared__ int s_row[kCcMaxB];                  // dataset rows of the client's batch
@@ -161,12 +161,12 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
 
     // ---- C: gradient, SGD update (M:303) and the client's row; thread = 2 features,
     // classes in groups of 16 (the batch columns are re-read per group from L1 / L2)
-    for (int c0 = 0; c0 < C; c0 += kCcCgC) {
-      float g[kCcFpt][kCcCgC];
+    for (int c0 = 0; c0 < C; c0 += CGC) {
+      float g[kCcFpt][CGC];
 #pragma unroll
       for (int h = 0; h < kCcFpt; ++h)
 #pragma unroll
-        for (int cc = 0; cc < kCcCgC; ++cc) g[h][cc] = 0.f;
+        for (int cc = 0; cc < CGC; ++cc) g[h][cc] = 0.f;
 #pragma unroll 2
       for (int s = 0; s < B; ++s) {
         float xv[kCcFpt];
@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
           }
         }
 #pragma unroll
-        for (int cc = 0; cc < kCcCgC; ++cc) {
+        for (int cc = 0; cc < CGC; ++cc) {
           const float dz = s_z[s][c0 + cc];              // (columns >= C: never stored)
 #pragma unroll
           for (int h = 0; h < kCcFpt; ++h) g[h][cc] = fmaf(dz, xv[h], g[h][cc]);
@@ -197,7 +197,7 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
         const int f = tid + kCcThreads * h;
         if (f < F) {
 #pragma unroll
-          for (int cc = 0; cc < kCcCgC; ++cc) {
+          for (int cc = 0; cc < CGC; ++cc) {
             const int c = c0 + cc;
             if (c < C) {
               float* wp = a.W + (int64_t)c * F + f;
@@ -232,14 +232,24 @@ hipError_t launch_client_chain(const ClientChainArgs& a, hipStream_t s) {
   // 13 features per lane: F <= 832 covers the reference's 28 x 28 inputs (MNIST and
   // EMNIST, F = 784) without idle iterations; 16 per lane spilled 164 VGPRs
   // the batch tile in LDS beside the 17 KB of s_z: up to 128 KB (B = 32 at F = 784: 98 KB)
+  // phase C's class groups: exactly C = 10 for MNIST's classifier (no padding classes: 16
+  // computed 6 never stored), 16 otherwise (EMNIST's 62: 4 groups)
   constexpr size_t kStageMax = 128u << 10;
-  static const bool stage_ok =   // the kernel's dynamic-LDS limit raised once per process
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&client_chain<kCcNj>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageMax) == hipSuccess;
+  auto raise = [](const void* fn) {   // the kernel's dynamic-LDS limit, once per process
+    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageMax) ==
+           hipSuccess;
+  };
+  static const bool ok10 = raise(reinterpret_cast<const void*>(&client_chain<kCcNj, 10>));
+  static const bool ok16 = raise(reinterpret_cast<const void*>(&client_chain<kCcNj, kCcCgC>));
+  const bool c10 = a.C <= 10;
   ClientChainArgs b = a;
   const size_t tile = (size_t)a.B * (size_t)a.F * sizeof(float);
-  b.stage = stage_ok && tile <= kStageMax ? 1 : 0;
-  hipLaunchKernelGGL(client_chain<kCcNj>, dim3(1), dim3(kCcThreads), b.stage ? tile : 0, s, b);
+  b.stage = (c10 ? ok10 : ok16) && tile <= kStageMax ? 1 : 0;
+  if (c10)
+    hipLaunchKernelGGL((client_chain<kCcNj, 10>), dim3(1), dim3(kCcThreads), b.stage ? tile : 0, s, b);
+  else
+    hipLaunchKernelGGL((client_chain<kCcNj, kCcCgC>), dim3(1), dim3(kCcThreads), b.stage ? tile : 0,
+                       s, b);
   return hipGetLastError();
 }
 
