@@ -907,14 +907,18 @@ def main():
             # block's partials plus the phases' VALU work.  Roofline: time per iteration
             # against the exchange floor (the kernel with its compute phases skipped, profiles/)
             us_it = avg_pass_s * 1e6 / max(res.iters, 1)
-            # (the floor on record is C2's own shape on rows; a panels call runs the batched
-            # kernel with P = 1, whose floor was measured at C5's shape only: not quoted)
+            # (the floor and the PMC traffic on record are C2's own shape on rows; a panels
+            # call of that shape runs the same kernel since round 4 session 2, not quoted)
             fl, fl_src = latency_floor("weiszfeld_resident") if layout == "rows" else (None, None)
             floor = fl["exchange_floor_us_per_iteration"] if fl else None
+            traffic, traffic_src = (pmc_traffic(args.workload, layout, "weiszfeld_resident")
+                                    if layout == "rows" and world == 1 else (None, None))
             roof = {"bound": "latency", "unit": "us per iteration", "achieved": us_it,
                     "peak": floor, "frac": floor / us_it if floor else None,
                     "frac_def": "exchange floor / achieved time per iteration (<= 1)",
-                    "floor_source": fl_src, "traffic": None,
+                    "floor_source": fl_src, "traffic": traffic,
+                    "traffic_unit": "GB per launch (PMC; X is 4*K*d bytes, read once)",
+                    "traffic_source": traffic_src,
                     "kernel": "weiszfeld_resident (every iteration in one launch, X in VGPRs)"
                               if layout == "rows" else "weiszfeld_resident_batched (P = 1)",
                     "launches_timed": launches, "avg_launch_us": avg_pass_s * 1e6,

@@ -569,5 +569,21 @@ r4s2q() {
   tail -2 $O/ab_c2.log
 }
 
+r4s2r() {
+  # C2's HBM traffic per launch (FETCH_SIZE / WRITE_SIZE, one counter per pass) with the
+  # L2-kept exchange (default) and with agent-scope stores over every XCD (GMAGG_RES_XCD=0);
+  # then the multi-rank rehearsals of r4s1n on the final code
+  O=gpurun_out/r4s2r; mkdir -p $O; export TMPDIR=/tmp
+  B="bench.py --workload c2 --steps 3 --warmup 1 --no-cpu --alt-steps 0 --no-check --soak 0"
+  for v in 2 0; do
+    for c in FETCH_SIZE WRITE_SIZE; do
+      GMAGG_RES_XCD=$v timeout -s KILL 200 rocprofv3 --pmc $c --output-format csv -d $O/x${v}_$c -o p -- python3 $B > $O/x${v}_$c.log 2>&1 || return 1
+    done
+    python3 tools/pmc_summary.py $O/x${v}_FETCH_SIZE/p_counter_collection.csv $O/x${v}_WRITE_SIZE/p_counter_collection.csv $O/pmc_x$v.json "c2 rows, GMAGG_RES_XCD=$v" > $O/summary_x$v.txt 2>&1 || return 2
+    grep -i resident $O/summary_x$v.txt | head -3
+  done
+  bash tools/gpu_sets.sh r4s1n
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
