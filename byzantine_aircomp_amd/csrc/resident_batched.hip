@@ -47,6 +47,9 @@ constexpr int kRbCols = 2048;                    // columns per block
 #ifndef GMK_RB_PREFETCH_ROWS
 #define GMK_RB_PREFETCH_ROWS 0
 #endif
+#ifndef GMK_RB_FASTCOEF
+#define GMK_RB_FASTCOEF 0   // A/B knob: the AirComp coefficients as resident.hip's (needs EARLY_H2)
+#endif
 // GMK_RB_EARLY_H2=1: the AirComp channel gains |h_k|^2 drawn in draw_pass, after the
 // previous publish, instead of inside the coefficient step on the iteration's dependent
 // chain: with the four-column noise blocks (philox.h normal1) C5 AirComp 803.6 -> 816.7
@@ -538,6 +541,25 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
           const double wk = kv ? 1.0 / (double)clamp_dist(d2k, a.eps) : 0.0;   // M:178
           const double Wsum = xlane_wave_sum(wk);
           if (k < KR) s_coef[w][k] = kv ? (float)(wk / Wsum) : 0.f;           // M:179
+        } else if (GMK_RB_FASTCOEF) {
+          // (resident.hip's fast coefficients: v_rcp / v_rsq, fp32 square roots and sums)
+          const float s = sqrtf((float)(gn2 * (1.0 / (double)d)));  // M:146
+          const float thr = (s * s) * 500.0f;                         // M:152
+          float ck = 0.f;
+          if (kv) {
+            const float d0 = sqrtf((float)d2k);
+            const float dist = d0 != d0 ? d0 : fmaxf(d0, a.eps);
+            const float pk = (s_rk[w][k] + s * s) *
+                             __builtin_amdgcn_rcpf(dist * dist * (float)(d + 1) * h2k);   // M:404
+            const float pup = pk != pk ? pk : fmaxf(pk, thr);          // M:405
+            ck = sqrtf((float)a.P_max) * __builtin_amdgcn_rsqf(pup) *
+                 __builtin_amdgcn_rcpf(dist);                          // M:407
+          }
+          const float Sc = xlane_wave_sum_f32(ck);
+          const float nd = !a.has_noise ? 0.f : (float)a.noise_sd * ndr;
+          const float scale = s * __builtin_amdgcn_rcpf(s * Sc + nd);   // M:153-155
+          if (k < KR) s_coef[w][k] = kv ? ck * scale : 0.f;
+          an = a.has_noise ? scale * (float)a.noise_sd : 0.f;
         } else {
           const float s = sqrtf((float)(gn2 / (double)d));          // M:146
           const float thr = (s * s) * 500.0f;                         // M:152

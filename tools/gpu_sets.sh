@@ -585,5 +585,27 @@ r4s2r() {
   bash tools/gpu_sets.sh r4s1n
 }
 
+r4s2s() {
+  # C5: the batched kernel's AirComp coefficients on v_rcp / v_rsq (fc: ALT_ONLY=
+  # resident_batched ALT_FLAGS=-DGMK_RB_FASTCOEF=1) on the AirComp reading; the OMA pre-noise
+  # drawn 4 (oma4) or 1 (oma1) rows at a time instead of 2 on the prenoise reading
+  O=gpurun_out/r4s2s; mkdir -p $O
+  GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_fc.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_resident_batched.py tests/test_gpu_c5_fullsize.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 2 --bench=--workload,c5,--reading,aircomp,--no-cpu,--alt-steps,0,--soak,0,--no-check,--steps,1,--warmup,0 --variant base= --variant fc=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_fc.so --out $O/ab_c5air.jsonl > $O/ab_c5air.log 2>&1 || { tail -20 $O/ab_c5air.log; return 2; }
+  tail -2 $O/ab_c5air.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 2 --bench=--workload,c5,--no-cpu,--alt-steps,0,--soak,0,--no-check --variant base= --variant oma4=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_oma4.so --variant oma1=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_oma1.so --out $O/ab_c5.jsonl > $O/ab_c5.log 2>&1 || { tail -20 $O/ab_c5.log; return 3; }
+  tail -3 $O/ab_c5.log
+}
+
+r4s2t() {
+  # C5 prenoise: the OMA pre-noise drawn 4 (oma4) or 1 (oma1) rows at a time instead of 2
+  O=gpurun_out/r4s2t; mkdir -p $O
+  GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_oma4.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_resident_batched.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 2 --bench=--workload,c5,--no-cpu,--alt-steps,0,--soak,0,--no-check --variant base= --variant oma4=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_oma4.so --variant oma1=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_oma1.so --out $O/ab_c5.jsonl > $O/ab_c5.log 2>&1 || { tail -20 $O/ab_c5.log; return 3; }
+  tail -3 $O/ab_c5.log
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
