@@ -112,7 +112,9 @@ int res_xcd_mode() {
   return e ? atoi(e) : 2;
 }
 unsigned res_xcd_stride(int nb, int num_cu) {
-  return (res_xcd_mode() != 0 && nb <= num_cu / 8) ? 8u : 1u;
+  // GMAGG_RES_XCD_BPC=n (A/B): up to n blocks per CU of the one XCD
+  static const int bpc = getenv("GMAGG_RES_XCD_BPC") ? std::max(1, atoi(getenv("GMAGG_RES_XCD_BPC"))) : 1;
+  return (res_xcd_mode() != 0 && nb <= num_cu / 8 * bpc) ? 8u : 1u;
 }
 // GMAGG_RB_XCD: 0 round-robin numbering, 1 XCD-major (default), 2 XCD-major with whole
 // groups per XCD whose granules stay in the XCD's L2 (resident_batched.hip rb_put)

@@ -666,6 +666,7 @@ static const void* resident_kernel(const PassCfg& cfg, int cpb) {
     switch (cpb) {                                                           \
       case 1: return res_fn<V_, W_, L_, R_, 1>();                            \
       case 2: return res_fn<V_, W_, L_, R_, 2>();                            \
+      case 3: return res_fn<V_, W_, L_, R_, 3>();                            \
       case 4: return res_fn<V_, W_, L_, R_, 4>();                            \
       case 8: return res_fn<V_, W_, L_, R_, 8>();                            \
       default: return nullptr;                                               \

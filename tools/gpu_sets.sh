@@ -607,5 +607,25 @@ r4s2t() {
   tail -3 $O/ab_c5.log
 }
 
+r4s2u() {
+  # C2's grid: 3 chunks per block (GMAGG_RES_CPB=3: 21 blocks of 384 columns) against 2
+  # (31 blocks, default); parity on it first
+  O=gpurun_out/r4s2u; mkdir -p $O
+  GMAGG_RES_CPB=3 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_weiszfeld.py -k "golden or gm_ or resident" > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant base= --variant cpb3=GMAGG_RES_CPB=3 --out $O/ab_c2.jsonl > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; return 2; }
+  tail -2 $O/ab_c2.log
+}
+
+r4s2v() {
+  # C2's grid: 1 chunk per block, 62 blocks, two per CU of the one XCD (GMAGG_RES_CPB=1
+  # GMAGG_RES_XCD_BPC=2) against 2 chunks per block (31 blocks, default)
+  O=gpurun_out/r4s2v; mkdir -p $O
+  GMAGG_RES_CPB=1 GMAGG_RES_XCD_BPC=2 GMAGG_RES_VERBOSE=1 timeout -k 10 200 python -u bench.py --workload c2 --no-cpu --alt-steps 0 --soak 0 --steps 3 --warmup 1 > $O/c2_b2.json 2> $O/c2_b2.err || { tail -20 $O/c2_b2.err; return 1; }
+  sort $O/c2_b2.err | uniq -c | head -4; cut -c1-200 $O/c2_b2.json
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant base= --variant "b2=GMAGG_RES_CPB=1;GMAGG_RES_XCD_BPC=2" --out $O/ab_c2.jsonl > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; return 2; }
+  tail -2 $O/ab_c2.log
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
