@@ -627,5 +627,15 @@ r4s2v() {
   tail -2 $O/ab_c2.log
 }
 
+r4s2w() {
+  # C2: thread 0's movement / ||g||^2 partial sums hoisted before phase B (product) against
+  # the previous kernel (libgmagg_alt_base.so: HEAD's resident.hip); parity first
+  O=gpurun_out/r4s2w; mkdir -p $O
+  timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_weiszfeld.py tests/test_gpu_panels.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 --variant base=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_base.so --variant fin= --out $O/ab_c2.jsonl > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; return 2; }
+  tail -2 $O/ab_c2.log
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
