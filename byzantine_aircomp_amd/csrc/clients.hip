@@ -84,6 +84,13 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
   const int F = (int)a.F, C = (int)a.C, B = (int)a.B;
   const float invB = 1.0f / (float)B;
 
+#ifdef GMK_CC_PROF
+  uint64_t prof_[4] = {0, 0, 0, 0};
+  uint64_t prev_ = __builtin_amdgcn_s_memrealtime();
+#define CC_T(i) if (tid == 0) { const uint64_t n_ = __builtin_amdgcn_s_memrealtime(); prof_[i] += n_ - prev_; prev_ = n_; }
+#else
+#define CC_T(i)
+#endif
   for (int64_t k = 0; k < a.K; ++k) {
     const bool byz = k >= a.honest;
     const bool flip_x = byz && a.attack == 2;
@@ -94,6 +101,7 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
       s_lab[tid] = (byz && a.attack == 1) ? (C - 1 - y) : y;
     }
     __syncthreads();
+    CC_T(0)
 
     // ---- A: logits.  The wave's batch tile: samples w + 8 i, features lane + 64 j
     float xr[kCcSpw][NJ];
@@ -146,6 +154,7 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
       }
     }
     __syncthreads();
+    CC_T(1)
 
     // ---- B: dz = d mean CE / dz, torch's log_softmax backward order
     for (int s = w; s < B; s += kCcWaves) {
@@ -158,10 +167,23 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
       if (cv) s_z[s][lane] = gout - expf(logp) * (-invB);
     }
     __syncthreads();
+    CC_T(2)
 
     // ---- C: gradient, SGD update (M:303) and the client's row; thread = 2 features,
     // classes in groups of 16 (the batch columns are re-read per group from L1 / L2)
     for (int c0 = 0; c0 < C; c0 += CGC) {
+      // the columns of W this thread updates, loaded before the sample loop (their latency
+      // hides behind it; loaded in the update loop they ran one round trip per element,
+      // each load ordered after the previous element's store to W): clamped addresses, no
+      // branches
+      float wold[kCcFpt][CGC];
+#pragma unroll
+      for (int h = 0; h < kCcFpt; ++h)
+#pragma unroll
+        for (int cc = 0; cc < CGC; ++cc) {
+          const int f = min(tid + kCcThreads * h, F - 1), c = min(c0 + cc, C - 1);
+          wold[h][cc] = a.W[(int64_t)c * F + f];
+        }
       float g[kCcFpt][CGC];
 #pragma unroll
       for (int h = 0; h < kCcFpt; ++h)
@@ -200,10 +222,9 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
           for (int cc = 0; cc < CGC; ++cc) {
             const int c = c0 + cc;
             if (c < C) {
-              float* wp = a.W + (int64_t)c * F + f;
-              const float p = *wp;
+              const float p = wold[h][cc];
               const float np = fmaf(-a.gamma, g[h][cc] + a.wd * p, p);
-              *wp = np;
+              a.W[(int64_t)c * F + f] = np;
               put_param(a, k, (int64_t)c * F + f, np);
             }
           }
@@ -220,7 +241,13 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
       put_param(a, k, (int64_t)C * F + c, np);
     }
     __syncthreads();   // W / b of this client before the next client's reads
+    CC_T(3)
   }
+#ifdef GMK_CC_PROF
+  if (tid == 0)
+    printf("GMK_CC_PROF K=%ld ns/client: setup %.0f A %.0f B %.0f C %.0f\n", (long)a.K,
+           10.0 * prof_[0] / a.K, 10.0 * prof_[1] / a.K, 10.0 * prof_[2] / a.K, 10.0 * prof_[3] / a.K);
+#endif
 }
 
 bool client_chain_supported(int64_t F, int64_t C, int64_t B) {
