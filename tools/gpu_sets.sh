@@ -637,5 +637,18 @@ r4s2w() {
   tail -2 $O/ab_c2.log
 }
 
+r4s2y() {
+  # kernel traces (rocprofv3 --kernel-trace --stats) of the default bench line (C3) and of the
+  # C5 and C4 lines on the final code, to pair each line's HIP-event timing with rocprof
+  O=gpurun_out/r4s2y; mkdir -p $O; export TMPDIR=/tmp
+  B="--no-cpu --alt-steps 0 --soak 0"
+  for w in "c3:" "c5:--workload c5" "c4:--workload c4 --steps 3 --warmup 1"; do
+    n=${w%%:*}; a=${w#*:}
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$n -o t -- python3 bench.py $a $B > $O/trace_$n.json 2> $O/trace_$n.err || return 1
+    head -4 $O/trace_$n/t_kernel_stats.csv | cut -c1-200
+    python3 -c "import json;l=json.load(open('$O/trace_$n.json'));print('$n bench avg_launch_us', l['roofline'].get('avg_launch_us'))"
+  done
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
