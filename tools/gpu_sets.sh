@@ -650,5 +650,19 @@ r4s2y() {
   done
 }
 
+r4s2x() {
+  # the single-problem resident kernel beyond C2's shape: the default 8-wave tile against the
+  # previous 16-wave one (GMAGG_RES_CFG=16,4), at d = 7,850 (one XCD), 20,000 and 48,670
+  # (the EMNIST MLP: grids too large for one XCD)
+  O=gpurun_out/r4s2x; mkdir -p $O
+  for r in 1 2; do
+    for v in default 16,4; do
+      if [ $v = default ]; then e=""; else e="GMAGG_RES_CFG=$v"; fi
+      env $e timeout -k 10 300 python -u tools/res_shape_bench.py >> $O/shapes.jsonl 2> $O/err.log || { tail -20 $O/err.log; return 1; }
+    done
+  done
+  cat $O/shapes.jsonl
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
