@@ -664,5 +664,19 @@ r4s2x() {
   cat $O/shapes.jsonl
 }
 
+r4s2aa() {
+  # the resident kernel's gather at large grids: 8 or 16 granules per poll round trip
+  # (libgmagg_alt_c8.so / _c16.so: ALT_ONLY=resident ALT_FLAGS=-DGMK_RES_NBCHUNK=8 / 16)
+  # against 4, at d = 7,850 / 20,000 / 48,670
+  O=gpurun_out/r4s2aa; mkdir -p $O
+  for r in 1 2; do
+    for v in base c8 c16; do
+      L=""; [ $v != base ] && L="GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt_$v.so"
+      env $L timeout -k 10 300 python -u tools/res_shape_bench.py --shapes 50x7850,50x20000,50x48670 | sed "s/}$/, \"lib\": \"$v\"}/" >> $O/shapes.jsonl 2> $O/err.log || { tail -20 $O/err.log; return 1; }
+    done
+  done
+  cat $O/shapes.jsonl | cut -c1-120
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
