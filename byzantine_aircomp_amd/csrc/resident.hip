@@ -16,10 +16,12 @@
 //   4. publishes its partials.
 // The exchange is the data itself: every per-block partial (D2_k, ||x_k||^2, the
 // movement and ||g||^2) is the block's fp64 sum rounded once to fp32 and carried by
-// ONE 8-byte {tag, fp32 value} granule written by one agent-scope relaxed
-// (write-through) store; readers poll the granules with agent-scope relaxed loads
-// until every tag equals the pass (cdna_hip_programming.md Guideline 16, R2), and
-// sum the blocks' values in fp64 in a fixed order.  No
+// ONE 8-byte {tag, fp32 value} granule written by one relaxed store — agent scope
+// (write-through), or, when the check-in finds every block on one XCD (C2's grid, round 4
+// session 2), workgroup scope, which keeps the line in that XCD's L2; readers poll the
+// granules with agent-scope relaxed loads (L2-served) until every tag equals the pass
+// (cdna_hip_programming.md Guideline 16, R2), and sum the blocks' values in fp64 in a
+// fixed order.  No
 // grid barrier, no release/acquire fences: the r1 version (62 one-chunk blocks,
 // counter barrier + fenced slab) spent 5.05 us of a 12.4 us iteration in the
 // barrier and 2.15 us in the slab reduction.  Passes alternate
