@@ -38,6 +38,16 @@
 
 namespace gmk {
 
+// Phase A's class-group loop unrolled at C <= 10 (3 groups of 4), so the next group's W
+// loads can be scheduled ahead of the current group's transpose (A/B knob)
+// Phase A's tile loads at clamped addresses, masked after the load (A/B knob)
+#ifndef GMK_CC_CLAMP
+#define GMK_CC_CLAMP 1
+#endif
+#ifndef GMK_CC_UNROLL_A
+#define GMK_CC_UNROLL_A 1
+#endif
+
 constexpr int kCcThreads = 512;
 constexpr int kCcWaves = kCcThreads / 64;
 constexpr int kCcSpw = 8;        // samples per wave in phase A (B <= 64)
@@ -46,6 +56,9 @@ constexpr int kCcFpt = 2;        // features per thread in phase C
 constexpr int kCcNj = 13;        // features per lane in phase A: F <= 832
 constexpr int kCcCgC = 16;       // classes per phase-C group (CGC: 10 when C <= 10)
 constexpr int kCcMaxC = 64;
+// dz row stride for phase C's class groups of CGC (C <= 10 with CGC = 10, else <= 64):
+// every column a group reads, rounded up to 16 bytes
+__host__ __device__ constexpr int cc_zs(int cgc) { return cgc == 10 ? 12 : 64; }
 constexpr int kCcMaxB = kCcWaves * kCcSpw;
 
 __device__ __forceinline__ void put_param(const ClientChainArgs& a, int64_t k, int64_t jj, float v) {
@@ -74,23 +87,64 @@ __device__ __forceinline__ float cc_wave_max(float v) {
 // sample), when B * F * 4 bytes fit (a.stage); else phase C reads global memory.
 template <int NJ, int CGC>
 __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a) {
-  __shared__ float s_z[kCcMaxB][kCcMaxC + 1];     // logits, then the gradient dz (padding 0)
   __shared__ int s_row[kCcMaxB];                  // dataset rows of the client's batch
   __shared__ int s_lab[kCcMaxB];                  // (relabelled) targets
-  extern __shared__ float s_x[];                  // [B][F] when a.stage
+  __shared__ float s_b[kCcMaxC];                  // the bias, read by phase A's logits
+  extern __shared__ float s_dyn[];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int F = (int)a.F, C = (int)a.C, B = (int)a.B;
   const float invB = 1.0f / (float)B;
+  // dynamic LDS: the logits, then the gradient dz, [B][ZS] (ZS: phase C's class groups
+  // covered, rounded up to 16-byte rows: its dz reads are 128-bit), then the batch tile
+  // [B][F] when a.stage
+  constexpr int ZS = cc_zs(CGC);
+  float* s_z = s_dyn;
+  float* s_x = s_dyn + B * ZS;
 
 #ifdef GMK_CC_PROF
-  uint64_t prof_[4] = {0, 0, 0, 0};
+  uint64_t prof_[5] = {0, 0, 0, 0, 0};
   uint64_t prev_ = __builtin_amdgcn_s_memrealtime();
 #define CC_T(i) if (tid == 0) { const uint64_t n_ = __builtin_amdgcn_s_memrealtime(); prof_[i] += n_ - prev_; prev_ = n_; }
 #else
 #define CC_T(i)
 #endif
+  // the wave's batch tile: samples w + 8 i, features lane + 64 j (rows by the sampler's
+  // index, s_row; 0 outside the batch).  (The row indices from LDS: read from global memory,
+  // which the kernel also writes, they are vector loads, and each one's wait drained every
+  // earlier row's loads: 8 round trips in sequence.)
+  float xr[kCcSpw][NJ];
+  auto load_tile = [&]() {
+    int rows[kCcSpw];
+#pragma unroll
+    for (int i = 0; i < kCcSpw; ++i) {
+      const int s = w + kCcWaves * i;
+      rows[i] = s < B ? s_row[s] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < kCcSpw; ++i) {
+      [[maybe_unused]] const int s = w + kCcWaves * i;
+      const float* row = a.data + (int64_t)rows[i] * a.ldd;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int f = lane + 64 * j;
+#if GMK_CC_CLAMP
+        xr[i][j] = row[min(f, F - 1)];   // every load issued, no branch; masked below
+#else
+        xr[i][j] = (s < B && f < F) ? row[f] : 0.f;
+#endif
+      }
+    }
+#if GMK_CC_CLAMP
+#pragma unroll
+    for (int i = 0; i < kCcSpw; ++i) {
+      const bool sv = w + kCcWaves * i < B;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) xr[i][j] = (sv && lane + 64 * j < F) ? xr[i][j] : 0.f;
+    }
+#endif
+  };
   for (int64_t k = 0; k < a.K; ++k) {
     const bool byz = k >= a.honest;
     const bool flip_x = byz && a.attack == 2;
@@ -100,21 +154,19 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
       const int y = (int)a.labels[r];
       s_lab[tid] = (byz && a.attack == 1) ? (C - 1 - y) : y;
     }
+    if (tid < C) s_b[tid] = a.b[tid];
     __syncthreads();
     CC_T(0)
 
-    // ---- A: logits.  The wave's batch tile: samples w + 8 i, features lane + 64 j
-    float xr[kCcSpw][NJ];
+    // ---- A: logits on the batch tile
+    load_tile();
+    if (flip_x) {
 #pragma unroll
-    for (int i = 0; i < kCcSpw; ++i) {
-      const int s = w + kCcWaves * i;
-      const float* row = a.data + (int64_t)(s < B ? s_row[s] : 0) * a.ldd;
+      for (int i = 0; i < kCcSpw; ++i) {
+        const int s = w + kCcWaves * i;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int f = lane + 64 * j;
-        float v = (s < B && f < F) ? row[f] : 0.f;
-        if (flip_x && s < B && f < F) v = 1.0f - v;        // M:326
-        xr[i][j] = v;
+        for (int j = 0; j < NJ; ++j)
+          if (s < B && lane + 64 * j < F) xr[i][j] = 1.0f - xr[i][j];   // M:326
       }
     }
     if (a.stage) {
@@ -128,7 +180,8 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
         }
       }
     }
-    for (int c0 = 0; c0 < C; c0 += kCcCg) {
+    CC_T(4)
+    auto logits = [&](const int c0) {
       float e[kCcSpw * kCcCg];                            // value i * CG + cc
 #pragma unroll
       for (int q = 0; q < kCcSpw * kCcCg; ++q) e[q] = 0.f;
@@ -150,8 +203,15 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
         const int v = row_of_lane<64, kCcSpw * kCcCg>(lane);
         const int i = v / kCcCg, cc = v % kCcCg;
         const int s = w + kCcWaves * i, c = c0 + cc;
-        if (s < B && c < C) s_z[s][c] = e[0] + a.b[c];
+        if (s < B && c < C) s_z[s * ZS + c] = e[0] + s_b[c];
       }
+    };
+    if constexpr (GMK_CC_UNROLL_A && CGC == 10) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+        if (g * kCcCg < C) logits(g * kCcCg);
+    } else {
+      for (int c0 = 0; c0 < C; c0 += kCcCg) logits(c0);
     }
     __syncthreads();
     CC_T(1)
@@ -159,12 +219,12 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
     // ---- B: dz = d mean CE / dz, torch's log_softmax backward order
     for (int s = w; s < B; s += kCcWaves) {
       const bool cv = lane < C;
-      const float z = cv ? s_z[s][lane] : -INFINITY;
+      const float z = cv ? s_z[s * ZS + lane] : -INFINITY;
       const float m = cc_wave_max(z);
       const float sum = xlane_wave_sum_f32(cv ? expf(z - m) : 0.f);
       const float logp = (z - m) - logf(sum);
       const float gout = (lane == s_lab[s]) ? -invB : 0.f;
-      if (cv) s_z[s][lane] = gout - expf(logp) * (-invB);
+      if (cv) s_z[s * ZS + lane] = gout - expf(logp) * (-invB);
     }
     __syncthreads();
     CC_T(2)
@@ -184,11 +244,13 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
           const int f = min(tid + kCcThreads * h, F - 1), c = min(c0 + cc, C - 1);
           wold[h][cc] = a.W[(int64_t)c * F + f];
         }
-      float g[kCcFpt][CGC];
+      float g[kCcFpt][CGC], gb[CGC];   // gb: the bias gradient (used by thread 0)
 #pragma unroll
-      for (int h = 0; h < kCcFpt; ++h)
+      for (int cc = 0; cc < CGC; ++cc) {
+        gb[cc] = 0.f;
 #pragma unroll
-        for (int cc = 0; cc < CGC; ++cc) g[h][cc] = 0.f;
+        for (int h = 0; h < kCcFpt; ++h) g[h][cc] = 0.f;
+      }
 #pragma unroll 2
       for (int s = 0; s < B; ++s) {
         float xv[kCcFpt];
@@ -209,7 +271,8 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
         }
 #pragma unroll
         for (int cc = 0; cc < CGC; ++cc) {
-          const float dz = s_z[s][c0 + cc];              // (columns >= C: never stored)
+          const float dz = s_z[s * ZS + c0 + cc];        // (columns >= C: never stored)
+          gb[cc] += dz;
 #pragma unroll
           for (int h = 0; h < kCcFpt; ++h) g[h][cc] = fmaf(dz, xv[h], g[h][cc]);
         }
@@ -230,23 +293,27 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
           }
         }
       }
-    }
-    if (tid < C) {
-      const int c = tid;
-      float gb = 0.f;
-      for (int s = 0; s < B; ++s) gb += s_z[s][c];
-      const float p = a.b[c];
-      const float np = fmaf(-a.gamma, gb + a.wd * p, p);
-      a.b[c] = np;
-      put_param(a, k, (int64_t)C * F + c, np);
+      if (tid == 0) {   // the bias: sum over s ascending, as the weights' gradients
+#pragma unroll
+        for (int cc = 0; cc < CGC; ++cc) {
+          const int c = c0 + cc;
+          if (c < C) {
+            const float p = s_b[c];
+            const float np = fmaf(-a.gamma, gb[cc] + a.wd * p, p);
+            a.b[c] = np;
+            put_param(a, k, (int64_t)C * F + c, np);
+          }
+        }
+      }
     }
     __syncthreads();   // W / b of this client before the next client's reads
     CC_T(3)
   }
 #ifdef GMK_CC_PROF
   if (tid == 0)
-    printf("GMK_CC_PROF K=%ld ns/client: setup %.0f A %.0f B %.0f C %.0f\n", (long)a.K,
-           10.0 * prof_[0] / a.K, 10.0 * prof_[1] / a.K, 10.0 * prof_[2] / a.K, 10.0 * prof_[3] / a.K);
+    printf("GMK_CC_PROF K=%ld ns/client: setup %.0f A-load/stage %.0f A-logits %.0f B %.0f C %.0f\n",
+           (long)a.K, 10.0 * prof_[0] / a.K, 10.0 * prof_[4] / a.K, 10.0 * prof_[1] / a.K,
+           10.0 * prof_[2] / a.K, 10.0 * prof_[3] / a.K);
 #endif
 }
 
@@ -258,25 +325,30 @@ bool client_chain_supported(int64_t F, int64_t C, int64_t B) {
 hipError_t launch_client_chain(const ClientChainArgs& a, hipStream_t s) {
   // 13 features per lane: F <= 832 covers the reference's 28 x 28 inputs (MNIST and
   // EMNIST, F = 784) without idle iterations; 16 per lane spilled 164 VGPRs
-  // the batch tile in LDS beside the 17 KB of s_z: up to 128 KB (B = 32 at F = 784: 98 KB)
   // phase C's class groups: exactly C = 10 for MNIST's classifier (no padding classes: 16
-  // computed 6 never stored), 16 otherwise (EMNIST's 62: 4 groups)
-  constexpr size_t kStageMax = 128u << 10;
+  // computed 6 never stored), 16 otherwise (EMNIST's 62: 4 groups).  Dynamic LDS: dz [B][ZS]
+  // and, when it fits beside it in the CU's 160 KB, the batch tile [B][F] (the reference's
+  // B = 50 at F = 784: 157 KB + 2.2 KB of dz at C = 10; EMNIST's C = 62 leaves no room)
+  constexpr size_t kLdsMax =   // (s_row, s_lab, s_b static)
+      (160u << 10) - 2 * kCcMaxB * sizeof(int) - kCcMaxC * sizeof(float);
   auto raise = [](const void* fn) {   // the kernel's dynamic-LDS limit, once per process
-    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageMax) ==
+    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax) ==
            hipSuccess;
   };
   static const bool ok10 = raise(reinterpret_cast<const void*>(&client_chain<kCcNj, 10>));
   static const bool ok16 = raise(reinterpret_cast<const void*>(&client_chain<kCcNj, kCcCgC>));
   const bool c10 = a.C <= 10;
-  ClientChainArgs b = a;
+  const int cgc = c10 ? 10 : kCcCgC;
+  const size_t zs = (size_t)cc_zs(cgc);
+  const size_t dz = (size_t)a.B * zs * sizeof(float);
   const size_t tile = (size_t)a.B * (size_t)a.F * sizeof(float);
-  b.stage = (c10 ? ok10 : ok16) && tile <= kStageMax ? 1 : 0;
+  ClientChainArgs b = a;
+  b.stage = (c10 ? ok10 : ok16) && dz + tile <= kLdsMax ? 1 : 0;
+  const size_t lds = dz + (b.stage ? tile : 0);
   if (c10)
-    hipLaunchKernelGGL((client_chain<kCcNj, 10>), dim3(1), dim3(kCcThreads), b.stage ? tile : 0, s, b);
+    hipLaunchKernelGGL((client_chain<kCcNj, 10>), dim3(1), dim3(kCcThreads), lds, s, b);
   else
-    hipLaunchKernelGGL((client_chain<kCcNj, kCcCgC>), dim3(1), dim3(kCcThreads), b.stage ? tile : 0,
-                       s, b);
+    hipLaunchKernelGGL((client_chain<kCcNj, kCcCgC>), dim3(1), dim3(kCcThreads), lds, s, b);
   return hipGetLastError();
 }
 

@@ -251,13 +251,17 @@ class _ClientChain:
         self.cuts = torch.tensor(cuts[:-1], dtype=torch.int32).unsqueeze(1)
         self.device = device
 
-    def step(self, streams, clients, honest, attack_name, gamma, wd):
+    @staticmethod
+    def draw(streams):
+        """One step's batch indices: the samplers' index lists, drawn in client order (a
+        RandomSampler seeds its generator from the global one at its first draw, M:260-270;
+        later draws touch only its own generator)."""
+        return torch.tensor([s._next_index() for s in streams], dtype=torch.int32)
+
+    def step(self, local, clients, honest, attack_name, gamma, wd):
         from . import _lib
         from .aggregators import _stream_ptr
-        K = len(streams)
-        # the samplers' index lists, drawn in client order (a RandomSampler seeds its
-        # generator from the global one at its first draw, M:260-270)
-        local = torch.tensor([s._next_index() for s in streams], dtype=torch.int32)
+        K = local.shape[0] if local.dim() == 2 else -1
         if local.shape != (K, self.B):
             raise RuntimeError("client batches must be full batches of batchSize samples")
         idx = (local + self.cuts).to(self.device, non_blocking=True)
@@ -338,12 +342,20 @@ def SGD(model, gamma, aggregate, weight_decay, noise_var=None, honestSize=0,  # 
         # our gm2 takes the pre-noise inside its first streaming pass (options
         # pre_oma_var: the same draws, seed drawn from torch's generator as OMA's is)
         fuse_oma = aggregate is _agg.gm2 and _agg._noise_source({}) == _agg._lib.GM_NOISE_PHILOX
+    steps_left = rounds * displayInterval
+    nxt = None
     for r in range(rounds):
         for _ in range(displayInterval):
             if chain is not None:
                 # the K clients' steps as one kernel (clients.hip): the same batches (the
-                # samplers' index streams, drawn in client order), the same chain
-                chain.step(streams, clients, honestSize, attack_name, gamma, weight_decay)
+                # samplers' index streams, drawn in client order), the same chain.  The
+                # next step's indices are drawn while the kernel and the aggregation run:
+                # the samplers are seeded by the first step's draws, so a later draw uses
+                # only its own generator and drawing it early changes no random stream
+                cur = nxt if nxt is not None else chain.draw(streams)
+                chain.step(cur, clients, honestSize, attack_name, gamma, weight_decay)
+                steps_left -= 1
+                nxt = chain.draw(streams) if steps_left > 0 else None
             for node in (range(K) if chain is None else ()):
                 xb, yb = next(streams[node])
                 xb, yb = xb.to(device), yb.to(device)

@@ -152,3 +152,40 @@ def test_client_kernel_rejects_mismatched_dataset():
     for y in (torch.arange(8) + 5, torch.arange(8) - 1, torch.zeros(8)):
         bad = torch.utils.data.TensorDataset(torch.zeros(8, 28, 28), y)
         assert "labels" in _ClientChain._unsupported(model, loss, bad, 4, 10)
+
+
+def test_client_kernel_predrawn_batches_keep_every_random_stream():
+    """training.SGD (client kernel) draws step t+1's batch indices while step t's kernel and
+    aggregation run.  Only the samplers' first draw touches the global generator (M:260-270:
+    RandomSampler seeds its own generator then), so drawing early must leave both the index
+    streams and the global stream (OMA seeds, evaluation iterators) exactly as in order."""
+    from byzantine_aircomp_amd import training as T
+    tr = torch.utils.data.TensorDataset(*synthetic_mnist(601, 400))
+    K, B, steps = 5, 10, 6
+
+    def streams():
+        n = len(tr)
+        cuts = [(i * n) // K for i in range(K + 1)]
+        sh = [torch.utils.data.Subset(tr, range(cuts[i], cuts[i + 1])) for i in range(K)]
+        return [iter(torch.utils.data.DataLoader(
+            sh[i], batch_size=B, sampler=torch.utils.data.RandomSampler(
+                sh[i], num_samples=steps * B, replacement=True))) for i in range(K)]
+
+    torch.manual_seed(7)
+    st = streams()
+    ref, g_ref = [], []
+    for _ in range(steps):
+        ref.append(T._ClientChain.draw(st))
+        g_ref.append(torch.randn(3))                 # a global-generator consumer per step
+    torch.manual_seed(7)
+    st = streams()
+    got, g_got, nxt = [], [], None
+    for t in range(steps):
+        cur = nxt if nxt is not None else T._ClientChain.draw(st)
+        nxt = T._ClientChain.draw(st) if t + 1 < steps else None
+        got.append(cur)
+        g_got.append(torch.randn(3))
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    for a, b in zip(g_ref, g_got):
+        assert torch.equal(a, b)

@@ -678,5 +678,67 @@ r4s2aa() {
   cat $O/shapes.jsonl | cut -c1-120
 }
 
+r4s3a() {
+  # the client chain (clients.hip): dz in dynamic LDS so the reference's B = 50 tile is
+  # staged (product: + the next client's tile prefetched behind phases B / C) against
+  # libgmagg_nopf.so (staged, no prefetch) and libgmagg_old.so (the previous kernel: B = 50
+  # not staged); then the phase probes (-DGMK_CC_PROF: _prof, _prof0, _profold)
+  O=gpurun_out/r4s3a; mkdir -p $O
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_training.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; return 1; }
+  tail -2 $O/tests.log
+  for r in 1 2; do
+    for v in base nopf old; do
+      L=""; [ $v != base ] && L="GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so"
+      env $L timeout -k 10 300 python -u tools/loop_bench.py --steps 20 | sed "s/}$/, \"lib\": \"$v\"}/" >> $O/loop.jsonl 2> $O/err.log || { tail -20 $O/err.log; return 2; }
+    done
+  done
+  for v in prof prof0 profold; do
+    GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so timeout -k 10 300 python -u tools/loop_bench.py --steps 5 > $O/$v.log 2>&1 || { tail -20 $O/$v.log; return 3; }
+    grep GMK_CC_PROF $O/$v.log | tail -3
+  done
+  cut -c1-60,150-260 $O/loop.jsonl
+}
+
+r4s3b() {
+  # the client chain: the product (staged B = 50 tile, bias in LDS, phase A's groups
+  # unrolled; the loop draws the next step's indices while the GPU runs) against
+  # libgmagg_nounroll.so (-DGMK_CC_UNROLL_A=0), _nopf (r4s3a's staged kernel) and _old (the
+  # kernel before r4s3a); the phase probe (-DGMK_CC_PROF)
+  O=gpurun_out/r4s3b; mkdir -p $O
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_training.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; return 1; }
+  tail -2 $O/tests.log
+  for r in 1 2; do
+    for v in base nounroll nopf old; do
+      L=""; [ $v != base ] && L="GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so"
+      env $L timeout -k 10 300 python -u tools/loop_bench.py --steps 20 | sed "s/}$/, \"lib\": \"$v\"}/" >> $O/loop.jsonl 2> $O/err.log || { tail -20 $O/err.log; return 2; }
+    done
+  done
+  for v in prof; do
+    GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so timeout -k 10 300 python -u tools/loop_bench.py --steps 5 > $O/$v.log 2>&1 || { tail -20 $O/$v.log; return 3; }
+    grep GMK_CC_PROF $O/$v.log | tail -3
+  done
+  cut -c1-60,150-260 $O/loop.jsonl
+}
+
+r4s3c() {
+  # the client chain: phase A's tile loads unconditional at clamped addresses, masked after
+  # (product) against libgmagg_noclamp.so (-DGMK_CC_CLAMP=0: per-load branches, a wait per
+  # row), _s3b (r4s3b's product) and _old (before r4s3a); phase probes _prof / _profnc
+  O=gpurun_out/r4s3c; mkdir -p $O
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_training.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; return 1; }
+  tail -2 $O/tests.log
+  for r in 1 2; do
+    for v in base noclamp s3b old; do
+      L=""; [ $v != base ] && L="GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so"
+      env $L timeout -k 10 300 python -u tools/loop_bench.py --steps 20 | sed "s/}$/, \"lib\": \"$v\"}/" >> $O/loop.jsonl 2> $O/err.log || { tail -20 $O/err.log; return 2; }
+    done
+  done
+  for v in prof profnc; do
+    GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so timeout -k 10 300 python -u tools/loop_bench.py --steps 5 > $O/$v.log 2>&1 || { tail -20 $O/$v.log; return 3; }
+    grep GMK_CC_PROF $O/$v.log | tail -3
+  done
+  cut -c1-60,150-260 $O/loop.jsonl
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
