@@ -38,12 +38,14 @@
 
 namespace gmk {
 
-// Phase A's class-group loop unrolled at C <= 10 (3 groups of 4), so the next group's W
-// loads can be scheduled ahead of the current group's transpose (A/B knob)
-// Phase A's tile loads at clamped addresses, masked after the load (A/B knob)
+// Phase A's tile loads at clamped addresses, masked after the load (A/B knob; 0: a branch
+// per load, and a wait per row)
 #ifndef GMK_CC_CLAMP
 #define GMK_CC_CLAMP 1
 #endif
+// Phase A's class-group loop unrolled at C <= 10 (3 groups of 4; A/B knob).  (Tried: the
+// next group's W columns loaded into registers before this group's transpose, or with the
+// batch tile: 358 VGPRs spilled)
 #ifndef GMK_CC_UNROLL_A
 #define GMK_CC_UNROLL_A 1
 #endif
@@ -104,7 +106,7 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
   float* s_x = s_dyn + B * ZS;
 
 #ifdef GMK_CC_PROF
-  uint64_t prof_[5] = {0, 0, 0, 0, 0};
+  uint64_t prof_[7] = {0, 0, 0, 0, 0, 0, 0};
   uint64_t prev_ = __builtin_amdgcn_s_memrealtime();
 #define CC_T(i) if (tid == 0) { const uint64_t n_ = __builtin_amdgcn_s_memrealtime(); prof_[i] += n_ - prev_; prev_ = n_; }
 #else
@@ -216,7 +218,30 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
     __syncthreads();
     CC_T(1)
 
-    // ---- B: dz = d mean CE / dz, torch's log_softmax backward order
+    // ---- B: dz = d mean CE / dz, torch's log_softmax backward order.  C <= 16 (the
+    // CGC = 10 kernel): four samples per wave, one 16-lane DPP row each (the 64-lane sums
+    // below add exact zeros above lane C, so the bits are the same)
+    if constexpr (CGC == 10) {
+      const int q = lane >> 4, cl = lane & 15;
+      for (int s0 = 4 * w; s0 < B; s0 += 4 * kCcWaves) {
+        const int s = s0 + q;
+        const bool cv = cl < C && s < B;
+        const float z = cv ? s_z[s * ZS + cl] : -INFINITY;
+        float m = z;
+        m = fmaxf(m, xlane_partner<8>(m));
+        m = fmaxf(m, xlane_partner<4>(m));
+        m = fmaxf(m, xlane_partner<2>(m));
+        m = fmaxf(m, xlane_partner<1>(m));
+        float sum = cv ? expf(z - m) : 0.f;
+        sum += xlane_partner<8>(sum);
+        sum += xlane_partner<4>(sum);
+        sum += xlane_partner<2>(sum);
+        sum += xlane_partner<1>(sum);
+        const float logp = (z - m) - logf(sum);
+        const float gout = (cv && cl == s_lab[s]) ? -invB : 0.f;
+        if (cv) s_z[s * ZS + cl] = gout - expf(logp) * (-invB);
+      }
+    } else
     for (int s = w; s < B; s += kCcWaves) {
       const bool cv = lane < C;
       const float z = cv ? s_z[s * ZS + lane] : -INFINITY;
@@ -277,6 +302,7 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
           for (int h = 0; h < kCcFpt; ++h) g[h][cc] = fmaf(dz, xv[h], g[h][cc]);
         }
       }
+      CC_T(5)
 #pragma unroll
       for (int h = 0; h < kCcFpt; ++h) {
         const int f = tid + kCcThreads * h;
@@ -305,15 +331,18 @@ __global__ void __launch_bounds__(kCcThreads, 1) client_chain(ClientChainArgs a)
           }
         }
       }
+      CC_T(6)
     }
     __syncthreads();   // W / b of this client before the next client's reads
     CC_T(3)
   }
 #ifdef GMK_CC_PROF
   if (tid == 0)
-    printf("GMK_CC_PROF K=%ld ns/client: setup %.0f A-load/stage %.0f A-logits %.0f B %.0f C %.0f\n",
+    printf("GMK_CC_PROF K=%ld ns/client: setup %.0f A-load/stage %.0f A-logits %.0f B %.0f "
+           "C-samples %.0f C-update %.0f C-end %.0f\n",
            (long)a.K, 10.0 * prof_[0] / a.K, 10.0 * prof_[4] / a.K, 10.0 * prof_[1] / a.K,
-           10.0 * prof_[2] / a.K, 10.0 * prof_[3] / a.K);
+           10.0 * prof_[2] / a.K, 10.0 * prof_[5] / a.K, 10.0 * prof_[6] / a.K,
+           10.0 * prof_[3] / a.K);
 #endif
 }
 
