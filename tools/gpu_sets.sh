@@ -740,5 +740,16 @@ r4s3c() {
   cut -c1-60,150-260 $O/loop.jsonl
 }
 
+r4s3z() {
+  # round 4 session 3 closing set: GPU suite + smoke + the default bench line
+  # (tools/final_check.sh), the training loop (product library) and its kernel trace
+  bash tools/final_check.sh || return $?
+  O=gpurun_out/r4s3z; mkdir -p $O
+  timeout -k 10 300 python -u tools/loop_bench.py --steps 20 > $O/loop.jsonl 2> $O/loop.err || { tail -20 $O/loop.err; return 2; }
+  cut -c1-60,150-260 $O/loop.jsonl
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_loop -o t -- python3 tools/loop_bench.py --steps 20 > $O/trace_loop.log 2>&1 || return 3
+  head -4 $O/trace_loop/t_kernel_stats.csv
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
