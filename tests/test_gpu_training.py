@@ -180,14 +180,16 @@ def _chain_reference(x, y, idx, W, b, honest, attack, gamma, wd, C):
 @pytest.mark.parametrize("C", [10, 62])
 @pytest.mark.parametrize("attack", [0, 1, 2])
 @pytest.mark.parametrize("layout", ["rows", "panels"])
-def test_client_chain_kernel_vs_fp64(C, attack, layout):
+@pytest.mark.parametrize("F", [784, 783])
+def test_client_chain_kernel_vs_fp64(C, attack, layout, F):
     """gm_client_chain_f32 (clients.hip) against the loop body in float64: every client's
-    row of the client matrix and the final W / b (the last client's, M:349)."""
+    row of the client matrix and the final W / b (the last client's, M:349).  F = 784 takes
+    the float2 phase-A kernel, odd F the scalar one."""
     import byzantine_aircomp_amd as bz
     from byzantine_aircomp_amd import _lib
     from byzantine_aircomp_amd.panels import ClientPanels
     g = torch.Generator().manual_seed(C * 10 + attack)
-    n, F, K, B, honest = 3000, 784, 12, 50, 9
+    n, K, B, honest = 3000, 12, 50, 9
     x = (0.3 * torch.randn(n, F, generator=g)).cuda()
     y = torch.randint(0, C, (n,), generator=g).cuda()
     idx = torch.randint(0, n, (K, B), generator=g, dtype=torch.int32).cuda()

@@ -751,5 +751,23 @@ r4s3z() {
   head -4 $O/trace_loop/t_kernel_stats.csv
 }
 
+r4s3d() {
+  # the client chain's phase A as float2 loads when F is even (product) against
+  # libgmagg_v1.so (-DGMK_CC_V2=0: the scalar slots); phase probes _prof / _prof1
+  O=gpurun_out/r4s3d; mkdir -p $O
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_training.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; return 1; }
+  tail -2 $O/tests.log
+  for r in 1 2 3; do
+    for v in base v1; do
+      L=""; [ $v != base ] && L="GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so"
+      env $L timeout -k 10 300 python -u tools/loop_bench.py --steps 20 | sed "s/}$/, \"lib\": \"$v\"}/" >> $O/loop.jsonl 2> $O/err.log || { tail -20 $O/err.log; return 2; }
+    done
+  done
+  for v in prof prof1; do
+    GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so timeout -k 10 300 python -u tools/loop_bench.py --steps 5 > $O/$v.log 2>&1 || { tail -20 $O/$v.log; return 3; }
+    grep GMK_CC_PROF $O/$v.log | tail -2
+  done
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
