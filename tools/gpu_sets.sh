@@ -769,5 +769,24 @@ r4s3d() {
   done
 }
 
+r4s3e() {
+  # the client chain's phase A reading W from LDS (copied once per client; product) against
+  # libgmagg_nowl.so (-DGMK_CC_WLDS=0: every wave loads the W columns from global memory);
+  # phase probes _prof / _profnw
+  O=gpurun_out/r4s3e; mkdir -p $O
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_training.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; return 1; }
+  tail -2 $O/tests.log
+  for r in 1 2 3; do
+    for v in base nowl; do
+      L=""; [ $v != base ] && L="GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so"
+      env $L timeout -k 10 300 python -u tools/loop_bench.py --steps 20 | sed "s/}$/, \"lib\": \"$v\"}/" >> $O/loop.jsonl 2> $O/err.log || { tail -20 $O/err.log; return 2; }
+    done
+  done
+  for v in prof profnw; do
+    GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so timeout -k 10 300 python -u tools/loop_bench.py --steps 5 > $O/$v.log 2>&1 || { tail -20 $O/$v.log; return 3; }
+    grep GMK_CC_PROF $O/$v.log | tail -2
+  done
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
