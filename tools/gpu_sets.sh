@@ -788,5 +788,19 @@ r4s3e() {
   done
 }
 
+r4s3f() {
+  # the client chain's next row / label loaded during phase C (product) against
+  # libgmagg_head.so (the setup's two dependent loads per client)
+  O=gpurun_out/r4s3f; mkdir -p $O
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_training.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; return 1; }
+  tail -2 $O/tests.log
+  for r in 1 2 3; do
+    for v in base head; do
+      L=""; [ $v != base ] && L="GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so"
+      env $L timeout -k 10 300 python -u tools/loop_bench.py --steps 20 | sed "s/}$/, \"lib\": \"$v\"}/" >> $O/loop.jsonl 2> $O/err.log || { tail -20 $O/err.log; return 2; }
+    done
+  done
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 "$1"
