@@ -802,6 +802,8 @@ r4s3f() {
   done
 }
 
+# (r4s3d-r4s3g: A/B sets of variants that were measured and not kept; their knobs are no
+# longer in clients.hip — DESIGN.md §3.5 records each result)
 r4s3g() {
   # the client chain's logits on f32 MFMA (product) against libgmagg_nomf.so
   # (-DGMK_CC_MFMA=0: the VALU dots); phase probe _prof
@@ -810,25 +812,6 @@ r4s3g() {
   tail -2 $O/tests.log
   for r in 1 2 3; do
     for v in base nomf; do
-      L=""; [ $v != base ] && L="GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so"
-      env $L timeout -k 10 300 python -u tools/loop_bench.py --steps 20 | sed "s/}$/, \"lib\": \"$v\"}/" >> $O/loop.jsonl 2> $O/err.log || { tail -20 $O/err.log; return 2; }
-    done
-  done
-  GMAGG_LIB=byzantine_aircomp_amd/libgmagg_prof.so timeout -k 10 300 python -u tools/loop_bench.py --steps 5 > $O/prof.log 2>&1 || { tail -20 $O/prof.log; return 3; }
-  grep GMK_CC_PROF $O/prof.log | tail -2
-}
-
-r4s3h() {
-  # the client chain's logits on f32 MFMA over the 8 waves, 4 accumulators, operands
-  # prefetched (libgmagg_mf.so, -DGMK_CC_MFMA=1) against the product (VALU dots); the
-  # training tests on the MFMA library; phase probe _prof (MFMA)
-  O=gpurun_out/r4s3h; mkdir -p $O
-  timeout -k 10 400 python -u -m pytest tests/test_gpu_training.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; return 1; }
-  tail -1 $O/tests.log
-  GMAGG_LIB=byzantine_aircomp_amd/libgmagg_mf.so timeout -k 10 400 python -u -m pytest tests/test_gpu_training.py -x -q --timeout 120 --timeout-method thread > $O/tests_mf.log 2>&1 || { tail -30 $O/tests_mf.log; return 1; }
-  tail -1 $O/tests_mf.log
-  for r in 1 2 3; do
-    for v in base mf; do
       L=""; [ $v != base ] && L="GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$v.so"
       env $L timeout -k 10 300 python -u tools/loop_bench.py --steps 20 | sed "s/}$/, \"lib\": \"$v\"}/" >> $O/loop.jsonl 2> $O/err.log || { tail -20 $O/err.log; return 2; }
     done
