@@ -12,7 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMAGG_LIB") or os.path.join(HERE, "libgmagg.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 GM_MODE_IDEAL, GM_MODE_AIRCOMP = 0, 1
 GM_NOISE_PHILOX, GM_NOISE_HOST = 0, 1
@@ -20,6 +20,7 @@ GM_ALGO_AUTO, GM_ALGO_STREAM, GM_ALGO_TWOPASS, GM_ALGO_GRAM, GM_ALGO_RESIDENT = 
 GM_ALGO_GRAM_F32 = 5
 GM_LAYOUT_ROWS, GM_LAYOUT_PANELS = 0, 1
 GM_GUARD_NONE, GM_GUARD_ACCEPTED, GM_GUARD_REJECTED, GM_GUARD_ACCEPTED_FLOOR = 0, 1, 2, 3
+GM_EXCHANGE_NONE, GM_EXCHANGE_AGENT, GM_EXCHANGE_XCD_LOCAL = 0, 1, 2
 
 NOISE_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.POINTER(C.c_float),
                        C.POINTER(C.c_float), C.POINTER(C.c_float))
@@ -56,6 +57,7 @@ class GmResult(C.Structure):
         ("algo_used", C.c_int32),
         ("guard", C.c_int32),
         ("gram_kind", C.c_int32),
+        ("exchange", C.c_int32),
     ]
 
 

@@ -58,6 +58,7 @@ class GMResult:
     algo: str
     guard: str = "none"      # Gram guard: "none", "accepted", "accepted_floor", "rejected"
     gram_kind: str = ""      # Gram runs: "f16_split", "bf16_split" (f16 range fallback), "f32"
+    exchange: str = "none"   # resident runs: "agent" (over XCDs) or "xcd_local" (one XCD's L2)
 
 
 last_result: GMResult | None = None
@@ -72,7 +73,8 @@ _GUARD_NAMES = {_lib.GM_GUARD_NONE: "none", _lib.GM_GUARD_ACCEPTED: "accepted",
 def _result(res) -> "GMResult":
     return GMResult(res.iters, res.last_movement, bool(res.converged),
                     _ALGO_NAMES.get(res.algo_used, "?"), _GUARD_NAMES.get(res.guard, "?"),
-                    {1: "f16_split", 2: "bf16_split", 3: "f32"}.get(res.gram_kind, ""))
+                    {1: "f16_split", 2: "bf16_split", 3: "f32"}.get(res.gram_kind, ""),
+                    {1: "agent", 2: "xcd_local"}.get(res.exchange, "none"))
 
 
 class Context:

@@ -16,7 +16,7 @@ import ctypes as C
 import torch
 
 from . import _lib
-from .aggregators import GMResult, _ALGOS, _ALGO_NAMES, _seed, _stream_ptr, context
+from .aggregators import GMResult, _ALGOS, _result, _seed, _stream_ptr, context
 from .panels import panel_width
 
 __all__ = ["gm2_batched", "gm_batched", "oma_batched", "ProblemPanels", "SEED_STRIDE"]
@@ -144,8 +144,7 @@ def _run(X, options: dict, aircomp: bool):
             out.data_ptr(), d, C.byref(o), res, _stream_ptr(X.device)), "gm_weiszfeld_batched_f32")
     if pre_var is not None and X is not X_in:
         X_in.copy_(X)          # the fused pre-noise is in place on the caller's problems
-    results = [GMResult(r.iters, r.last_movement, bool(r.converged),
-                        _ALGO_NAMES.get(r.algo_used, "?")) for r in res]
+    results = [_result(r) for r in res]
     return out, results
 
 

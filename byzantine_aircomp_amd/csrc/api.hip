@@ -413,6 +413,7 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   r.last_movement = hst->last_movement;
   r.converged = hst->converged;
   r.algo_used = GM_ALGO_RESIDENT;
+  r.exchange = hbar[0] == 2 ? GM_EXCHANGE_XCD_LOCAL : GM_EXCHANGE_AGENT;   // bar[0] = 1 + local
   if (res) *res = r;
   return GM_OK;
 }
@@ -524,7 +525,9 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
   if (results)
     for (int64_t p = 0; p < P; ++p)
       results[p] = gm_result{hst[p].iters, hst[p].last_movement, hst[p].converged,
-                             GM_ALGO_RESIDENT, GM_GUARD_NONE, 0};
+                             GM_ALGO_RESIDENT, GM_GUARD_NONE, 0,
+                             hflag[1] == (unsigned)plan.ng ? GM_EXCHANGE_XCD_LOCAL
+                                                           : GM_EXCHANGE_AGENT};
   return GM_OK;
 }
 

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GMAGG_ABI_VERSION 3
+#define GMAGG_ABI_VERSION 4
 
 enum gm_status {
     GM_OK = 0,
@@ -126,6 +126,13 @@ enum gm_guard {
                                  count is decided by rounding there; iters is the exact count */
 };
 
+enum gm_exchange {
+    GM_EXCHANGE_NONE = 0,      /* launch-per-pass paths: partials reduced between launches */
+    GM_EXCHANGE_AGENT = 1,     /* resident grid over several XCDs: agent-scope granule stores */
+    GM_EXCHANGE_XCD_LOCAL = 2  /* resident grid on ONE XCD (confirmed from XCC_ID at the
+                                  check-in): granules kept in that XCD's L2 */
+};
+
 typedef struct gm_result {
     int64_t iters;            /* Weiszfeld loop bodies executed (M:145 / M:173) */
     double last_movement;     /* ||guess_t - guess_{t+1}|| of the last body (M:156 / M:180) */
@@ -134,6 +141,8 @@ typedef struct gm_result {
     int32_t guard;            /* gm_guard: what the Gram accuracy guard decided */
     int32_t gram_kind;        /* Gram runs: 1 scaled f16 split (3 MFMA products), 2 bf16 split
                                  (4 products, after an f16 range overflow), 3 f32-input; else 0 */
+    int32_t exchange;         /* register-resident runs: how the blocks exchanged their
+                                 per-iteration partials (gm_exchange); else GM_EXCHANGE_NONE */
 } gm_result;
 
 typedef struct gm_ctx gm_ctx;
