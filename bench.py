@@ -280,6 +280,27 @@ def cpu_baseline(X, g0, agg, var, iters, d_full, budget, max_cols):
                        + ("" if dc == d_full else ", linear in d (extrapolated)"))}
 
 
+def c5_rank_slice(per_var: int, world: int, rank: int):
+    """Rank `rank`'s contiguous share [q0, q1) of a var group's `per_var` problems (the
+    first per_var % world ranks take one more)."""
+    base, extra = divmod(per_var, world)
+    q0 = rank * base + min(rank, extra)
+    return q0, q0 + base + (1 if rank < extra else 0)
+
+
+def c5_seed(vi: int, q: int) -> int:
+    """Data seed of problem q of var group vi (its index in the whole sweep, any N)."""
+    return 1_000_003 * vi + q
+
+
+def c5_draw_seed(vi: int, c0: int) -> int:
+    """Draw seed of a batched call whose first problem is q = c0 of var group vi: the
+    library keys problem p of the call seed + p * SEED_STRIDE (batched.py), so problem q
+    is keyed 31 + 1000 vi + q * SEED_STRIDE whichever rank and chunk run it."""
+    from byzantine_aircomp_amd.batched import SEED_STRIDE
+    return (31 + 1000 * vi + c0 * SEED_STRIDE) % 2 ** 64
+
+
 def run_c5(args, json_out, rank=0, world=1):
     """BASELINE config C5: a draw.ipynb-style Monte-Carlo sweep of `args.problems`
     independent K=50 x d=100k aggregations over var in {0, 1e-3, 1e-2, 1e-1} x
@@ -289,10 +310,11 @@ def run_c5(args, json_out, rank=0, world=1):
     pre-noise (M:385-394) first — both inside the timed region.  Inputs are
     regenerated on the device (untimed) before every step, since OMA is in place.
 
-    N > 1 (problems sharded over GPUs): every rank runs its own sweep of
-    `args.problems` problems (seeds offset by rank; no collective on the data path, a
-    gloo barrier and max-over-ranks timing around each step): weak scaling, value = all
-    ranks' problems / the slowest rank's time."""
+    N > 1 (the sweep's problems sharded over GPUs): rank r runs its
+    contiguous share of every var group (c5_rank_slice), each problem keyed by its index
+    in the WHOLE sweep, so a problem's data, draws and result do not depend on N; no
+    collective on the data path, a gloo barrier and max-over-ranks timing around each
+    step: strong scaling, value = the sweep's problems / the slowest rank's time."""
     import byzantine_aircomp_amd as bz
     from byzantine_aircomp_amd import _lib
     from byzantine_aircomp_amd.batched import gm2_batched, gm_batched, oma_batched
@@ -303,12 +325,15 @@ def run_c5(args, json_out, rank=0, world=1):
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-    rs = rank * 1_000_003                       # this rank's problems: other seeds
     K, d, _, _, _ = WORKLOADS["c5"]
     ctx = bz.context(dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
     per_var = args.problems // len(C5_VARS)
-    chunk = max(1, min(args.c5_batch, per_var))
+    q0, q1 = c5_rank_slice(per_var, world, rank)      # this rank's share of every var group
+    chunk = max(1, min(args.c5_batch, q1 - q0))
+    # the guesses of a chunk are one fill keyed by the problems' index in the whole sweep
+    # (a context whose shard offset is that index x d), so they do not depend on N
+    gctx = bz.aggregators.Context(dev.index)
     # layout: the batched problems in the panel layout (ProblemPanels: every chunk one
     # contiguous block, as for C3) unless --layout rows; the panels are packed from the
     # row-major fill, untimed
@@ -320,8 +345,8 @@ def run_c5(args, json_out, rank=0, world=1):
     groups = []
     tmp = torch.empty(K, d, device=dev) if use_panels else None
     for vi, var in enumerate(C5_VARS):
-        for c0 in range(0, per_var, chunk):
-            P = min(chunk, per_var - c0)
+        for c0 in range(q0, q1, chunk):             # c0: the chunk's first problem in the group
+            P = min(chunk, q1 - c0)
             groups.append((vi, var, c0, None if use_panels else torch.empty(P, K, d, device=dev),
                            torch.empty(P, d, device=dev),
                            ProblemPanels(P, K, d, device=dev) if use_panels else None))
@@ -332,7 +357,7 @@ def run_c5(args, json_out, rank=0, world=1):
     def fill_problem(vi, c0, p, dst, g0p, recipe):
         """Problem p's [K, d] rows into dst (its guess g0p already filled)."""
         B = C5_BYZ[(c0 + p) % 3]
-        seed = rs + 1000 * vi + c0 + p
+        seed = c5_seed(vi, c0 + p)
         if recipe == "outlier":
             _lib.check(ctx.lib.gm_fill_clients_f32(ctx.handle, dst.data_ptr(), K, d, d, B, 0.0,
                                                    0.05, 0.25, 0.5, seed, stream), "fill")
@@ -344,9 +369,10 @@ def run_c5(args, json_out, rank=0, world=1):
     def fill(reading):
         recipe = recipe_of(reading)
         for vi, var, c0, X, g0, Pn in groups:
-            _lib.check(ctx.lib.gm_fill_normal_f32(ctx.handle, g0.data_ptr(), g0.numel(), 0.0,
+            gctx.set_shard(per_var * d, c0 * d)
+            _lib.check(ctx.lib.gm_fill_normal_f32(gctx.handle, g0.data_ptr(), g0.numel(), 0.0,
                                                   0.01 if recipe == "outlier" else 0.07,
-                                                  rs + 777 + vi + c0, stream), "fill")
+                                                  777 + vi, stream), "fill")
             for p in range(g0.shape[0]):
                 if Pn is None:
                     fill_problem(vi, c0, p, X[p], g0[p], recipe)
@@ -368,14 +394,14 @@ def run_c5(args, json_out, rank=0, world=1):
             if var == 0.0:
                 out, res = gm2_batched(X, opts)
             elif reading == "prenoise" and args.separate_oma:
-                oma_batched(X, var, seed=rs + 31 + vi * 1000 + c0)
+                oma_batched(X, var, seed=c5_draw_seed(vi, c0))
                 out, res = gm2_batched(X, opts)
             elif reading == "prenoise":
                 # the pre-noise fused into gm2's first pass (same draws as oma_batched)
                 out, res = gm2_batched(X, dict(opts, pre_oma_var=var,
-                                               pre_oma_seed=rs + 31 + vi * 1000 + c0))
+                                               pre_oma_seed=c5_draw_seed(vi, c0)))
             else:
-                out, res = gm_batched(X, dict(opts, noise_var=var, seed=rs + 31 + vi * 1000 + c0))
+                out, res = gm_batched(X, dict(opts, noise_var=var, seed=c5_draw_seed(vi, c0)))
             outs[(vi, c0)] = (out, res)
             torch.cuda.synchronize(dev)
             dt = time.perf_counter() - t0
@@ -415,7 +441,8 @@ def run_c5(args, json_out, rank=0, world=1):
     total, pass_ms, launches, iters, per_group = measure(args.reading, args.steps, args.warmup)
     check = c5_check(groups, outs, args.reading, args.maxiter, recipe_of(args.reading)) \
         if not args.no_check else None
-    n_prob = len(iters)
+    n_prob = len(iters)                          # this rank's problems
+    n_total = per_var * len(C5_VARS)             # the sweep's, over every rank
     mean_it = sum(iters) / n_prob
     step_bytes = sum(iters) * 4.0 * K * d            # algorithmic STEP-pass bytes per sweep
     achieved = step_bytes * args.steps / (pass_ms / 1e3) / 1e9 if pass_ms > 0 else None
@@ -512,27 +539,29 @@ def run_c5(args, json_out, rank=0, world=1):
         cpu = c5_cpu_baseline(tmp if X0 is None else X0[0], g00[0], mean_it, n_prob,
                               args.cpu_budget)
     line = {
-        "metric": METRIC, "value": world * n_prob * args.steps / total, "unit": "aggregations/s",
+        "metric": METRIC, "value": n_total * args.steps / total, "unit": "aggregations/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": 1e3 * total / args.steps, "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": 1e3 * total / args.steps, "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None, "dtype": "f32",
         "data": ("synthetic (Philox on device: honest N(0,0.05^2), B rows N(0.25,0.5^2), "
                  "guess N(0,0.01^2))" if recipe_of(args.reading) == "outlier" else
                  "synthetic (Philox on device, the reference's caller M:349: guess = model p ~ "
                  "N(0,0.07^2), honest rows p + N(0,(5e-4)^2), B rows p + 2e-3 + N(0,(5e-3)^2))"),
-        "config": {"workload": f"c5: {n_prob} independent gm2 problems K={K} x d={d} fp32 over "
+        "config": {"workload": f"c5: {n_total} independent gm2 problems K={K} x d={d} fp32 over "
                                f"var {list(C5_VARS)} x B {list(C5_BYZ)}, reading '{args.reading}'"
                                + ((" (OMA pre-noise then gm2, M:351-353; separate OMA pass)"
                                    if args.separate_oma else
                                    " (OMA pre-noise then gm2, M:351-353; the pre-noise fused "
                                    "into gm2's first pass)")
                                   if args.reading == "prenoise" else " (AirComp gm for var > 0)"),
-                   "K": K, "d": d, "problems": n_prob, "mean_iters": mean_it, "batch": chunk,
+                   "K": K, "d": d, "problems": n_total, "problems_per_rank": n_prob,
+                   "mean_iters": mean_it, "batch": chunk,
                    "algo": algo_used, "recipe": recipe_of(args.reading),
                    "parallelism": ("register-resident batched (one launch per group: each problem "
                                    "held on chip for all its iterations)" if algo_used == "resident"
                                    else "batched (one launch per pass covers every problem of a group)")
-                                  + (f"; problems sharded over {world} GPUs (each rank its own "
+                                  + (f"; the sweep's problems sharded over {world} GPUs (rank 0: "
                                      f"{n_prob}; no data-path collective)" if world > 1 else ""),
                    "layout": "panels (ProblemPanels)" if use_panels else "rows",
                    "groups": {str(k): {"problems_per_s": v["problems"] / v["seconds"],
@@ -666,8 +695,69 @@ def c5_cpu_baseline(X, g0, mean_iters, problems, budget):
                       f"problem (the sweep's mean); {problems} problems take {problems * per_problem:.0f} s"}
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv, cmd=None, poll_s: float = 0.2) -> int:
+    """`python bench.py --gpus N` with N > 1 and no launcher around it (no WORLD_SIZE in
+    the environment): start N fresh worker processes of this script, one per GPU, with
+    RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR (127.0.0.1) /
+    MASTER_PORT set — exactly what `torch.distributed.run --nproc-per-node N` gives them —
+    relay rank 0's one JSON line to stdout, and return non-zero if any rank fails (the
+    other ranks are then stopped, by their own PIDs, so none waits at a barrier forever).
+    This process makes no GPU call: it only spawns and waits.  `cmd` replaces the worker
+    command line (tests)."""
+    import subprocess
+    cmd = cmd or [sys.executable, os.path.abspath(__file__), *argv]
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else
+                                      subprocess.DEVNULL))
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench.py launcher: rank {r} exited with {c}; stopping the others",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    procs[q].terminate()
+        if live:
+            time.sleep(poll_s)
+    for p in procs:
+        p.wait()
+    out = procs[0].stdout.read().decode(errors="replace") if procs[0].stdout else ""
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    if lines:
+        sys.stdout.write(lines[-1] + "\n")
+        sys.stdout.flush()
+    elif rc == 0:
+        print("bench.py launcher: rank 0 printed no result line", file=sys.stderr)
+        rc = 1
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver's plain `python bench.py --gpus N`: become the launcher (before any GPU
+        # call; counting devices does not initialise the GPU on this image)
+        if not args.one_gpu and torch.cuda.device_count() < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but {torch.cuda.device_count()} GPU(s) visible")
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
     if os.environ.get("BENCH_EXIT_MAPS"):
         # diagnostics: this process's memory map as the interpreter exits, to attribute
         # the PCs of a crash in the C-level exit handlers to their DSOs

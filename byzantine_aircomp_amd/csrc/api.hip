@@ -83,7 +83,9 @@ namespace {
 
 constexpr int kResSkipAfterCheckinFail = 64;
 
-// Resident paths are tried unless a recent call's grid failed its check-in.
+// Resident paths are tried unless a recent call's grid failed its check-in.  Called ONCE
+// per public call (gm_weiszfeld_f32, gm_weiszfeld_batched_f32), so the skip window lasts
+// kResSkipAfterCheckinFail calls however many resident paths a call considers.
 bool resident_allowed(gm_ctx* c) {
   if (c->res_skip <= 0) return true;
   --c->res_skip;
@@ -427,14 +429,14 @@ constexpr int kRbNotTaken = 1;
 int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_t d,
                          int64_t ldx, int64_t ldp, bool panels, int64_t Wp, const float* guess0,
                          int64_t ldg, float* out, int64_t ldo, const gm_opts* o,
-                         gm_result* results, hipStream_t s) {
+                         gm_result* results, hipStream_t s, bool res_ok) {
   static const bool on = [] {
     const char* e = getenv("GMAGG_BATCH_RESIDENT");
     return !(e && atoi(e) == 0);
   }();
   if (!on || c->d_total > 0) return kRbNotTaken;
   if (o->mode == GM_MODE_AIRCOMP && o->noise_source != GM_NOISE_PHILOX) return kRbNotTaken;
-  if (!resident_allowed(c)) return kRbNotTaken;
+  if (!res_ok) return kRbNotTaken;   // (resident_allowed, taken once by the caller)
   // float4 tile rows: 16-byte aligned problems, rows and panels
   if ((reinterpret_cast<uintptr_t>(X) & 15) || ldp % 4 || ldx % 4 || (panels && Wp % 4))
     return kRbNotTaken;
@@ -637,7 +639,7 @@ again:
     rho = rho != rho ? 0.5 : std::min(0.95, std::max(0.5, rho));
     const double pred = hst->guard_q / (1.0 - rho) / gn;
     const bool accurate = pred <= 1e-6;                     // NaN fails
-    const double floor = 2.0 * u * gn;
+    const double floor = kFloorUlps * u * gn;        // (oracle FLOOR_ULPS, the count window)
     const bool floor_ok = !hst->converged || floor <= o->tol;
     floor_band = hst->converged && floor > o->tol / 3.0;
     static const bool dbg = getenv("GMAGG_GUARD_DEBUG") != nullptr;
@@ -821,6 +823,8 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   // Algorithm and tile.
   PassCfg cfg{};
   int algo = o->algo;
+  // (a recursive call on the staged panel copy is the same call: no second turn)
+  const bool res_ok = o->algo == GM_ALGO_STREAM || resident_allowed(c);
   bool panel_gram_rejected = false;
   const bool panels = o->layout == GM_LAYOUT_PANELS;
   if (o->layout != GM_LAYOUT_ROWS && !panels)
@@ -859,7 +863,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
     // iterations.
     const bool host_noise = o->mode == GM_MODE_AIRCOMP && o->noise_source == GM_NOISE_HOST;
     if ((algo == GM_ALGO_AUTO || algo == GM_ALGO_RESIDENT) && !sharded && !c->comm && !c->ar_fn &&
-        !host_noise && K <= 64 && resident_allowed(c)) {
+        !host_noise && K <= 64 && res_ok) {
       PassCfg rcfg{};
       int cpb = 0, nbr = 0;
       int ws = 0;
@@ -879,7 +883,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
     }
     if ((algo == GM_ALGO_AUTO || algo == GM_ALGO_RESIDENT) && !sharded && !c->comm && !c->ar_fn) {
       const int rc0 = run_resident_batched(c, X, 1, K, d, ldx, (d + W - 1) / W * ldx, true, W,
-                                           guess0, d, out, d, o, res, s);
+                                           guess0, d, out, d, o, res, s, res_ok);
       if (rc0 != kRbNotTaken) return rc0;
     }
     if (algo == GM_ALGO_AUTO) algo = GM_ALGO_STREAM;
@@ -924,7 +928,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
     const int J = cfg.LPR * cfg.V;
     const int64_t nch = (d + J - 1) / J;
     int cpb = 0, nbr = 0;
-    if (resident_allowed(c) && resident_plan(cfg, nch, c->num_cu, &cpb, &nbr)) {
+    if (res_ok && resident_plan(cfg, nch, c->num_cu, &cpb, &nbr)) {
       bool timed_out = false;
       int rco = apply_oma();
       if (rco) return rco;
@@ -1226,7 +1230,7 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
   // reads each problem's X once (resident_batched.hip); AUTO or GM_ALGO_RESIDENT
   if (o->maxiter > 0 && (o->algo == GM_ALGO_AUTO || o->algo == GM_ALGO_RESIDENT)) {
     const int rcr = run_resident_batched(c, X, P, K, d, ldx, ldp, panels, Wp, guess0, ldg, out,
-                                         ldo, o, results, s);
+                                         ldo, o, results, s, resident_allowed(c));
     if (rcr != kRbNotTaken) return rcr;
   }
   if (o->algo == GM_ALGO_RESIDENT)

@@ -63,6 +63,11 @@ struct PassArgs {
 };
 
 constexpr uint64_t kSeedStride = 0x9E3779B97F4A7C15ull;
+// The reference's fp32 movement floor in ulps of ||g|| (M:180: an fp32 norm of a difference
+// of fp32 iterates): the Gram guard accepts an exact-arithmetic count only where
+// kFloorUlps * 2^-24 * ||g|| <= tol.  The SAME constant as oracle/aggregators.py FLOOR_ULPS
+// (the count window the tests check counts against; measured: profiles/r5s1_movement_floor.txt)
+constexpr double kFloorUlps = 2.0;
 
 struct KspaceArgs {
   int64_t K, d_total, t;  // t = pass just completed, -1 after the initial pass

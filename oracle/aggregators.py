@@ -179,21 +179,34 @@ def gm2_f64(X: torch.Tensor, guess: torch.Tensor, maxiter: int = 200, tol: float
     return g, WeiszfeldTrace(n, moved)
 
 
+# The fp32 movement floor, in ulps of ||g||: an fp32 Weiszfeld's computed movement differs
+# from the exact one by about this much (profiles/r5s1_movement_floor.txt: <= 2.0 ulps at the
+# tol crossing on every C4-recipe input, 0.6-1.0 ulps at the fixed point).  The SAME constant
+# as the Gram guard's floor rule (byzantine_aircomp_amd/csrc/gmagg_internal.h kFloorUlps,
+# api.hip run_gram; tests/test_iteration_wellposed.py checks the two agree).
+FLOOR_ULPS = 2.0
+
+
 @dataclass
 class CountWindow:
     """The iteration counts an fp32 Weiszfeld may legitimately stop at on one input."""
 
     early: int            # first t whose fp64 movement is <= tol + delta_t
-    late: int             # first t whose fp64 movement is <= tol - delta_t (maxiter if none)
+    late: Optional[int]   # first t whose fp64 movement is <= tol - delta_t (maxiter if none);
+                          # None = undetermined: tol - delta <= 0, no count is certain
     max_norm: float       # max ||g_t|| over the run (sets the fp32 movement floor)
 
     @property
-    def width(self) -> int:
-        return self.late - self.early
+    def determined(self) -> bool:
+        return self.late is not None
+
+    @property
+    def width(self) -> Optional[int]:
+        return None if self.late is None else self.late - self.early
 
 
 def gm2_count_window(X: torch.Tensor, guess: Optional[torch.Tensor] = None, maxiter: int = 200,
-                     tol: float = 1e-5, floor_ulps: float = 4.0) -> CountWindow:
+                     tol: float = 1e-5, floor_ulps: float = FLOOR_ULPS) -> CountWindow:
     """Is "the same iteration count +-1" (north_star) well posed on this input?
 
     The reference stops at the first t with ||g_t - g_{t+1}|| <= tol (M:180-183), on
@@ -203,12 +216,17 @@ def gm2_count_window(X: torch.Tensor, guess: Optional[torch.Tensor] = None, maxi
     count between ``early`` (exact movement <= tol + delta) and ``late`` (exact
     movement <= tol - delta) is then a legitimate stopping point, for the reference as
     for a kernel: two fp32 implementations agree to +-1 only if ``late - early <= 1``.
-    A wider window means tol sits on the fp32 movement floor and the count measures
-    rounding, not the algorithm (6 vs 8 at ||g|| ~ 8, tol 1e-6).
-    Runs the exact (fp64) iteration until the movement is below tol - delta."""
+    A wider window means tol sits near the fp32 movement floor and the count measures
+    rounding, not the algorithm (6 vs 8 at ||g|| ~ 8, tol 1e-6).  When
+    tol - delta <= 0 the window is UNDETERMINED (``late`` None): an fp32 run may never
+    see a movement below tol (it stops only if rounding happens to land it there, or on
+    an exact fixed point of its own arithmetic), so no count is certain and a test must
+    state its own bar.  Runs the exact (fp64) iteration until the movement is below
+    tol - delta."""
     X64 = X.double()
     g = (X64.mean(dim=0) if guess is None else guess.double())
     early = late = None
+    undetermined = False
     max_norm = float(torch.linalg.vector_norm(g))
     for t in range(1, maxiter + 1):
         dist = torch.clamp(torch.linalg.vector_norm(X64 - g, dim=1), min=CLAMP)
@@ -223,8 +241,13 @@ def gm2_count_window(X: torch.Tensor, guess: Optional[torch.Tensor] = None, maxi
         if moved <= tol - delta:
             late = t
             break
-        if not math.isfinite(moved) or (early is not None and tol - delta <= 0):
-            break                   # (tol below the floor: no count is certain)
+        if not math.isfinite(moved):
+            break                   # NaN never passes the test: both run to maxiter
+        if early is not None and tol - delta <= 0:
+            undetermined = True     # (tol below the floor: no count is certain)
+            break
     early = maxiter if early is None else early
+    if undetermined:
+        return CountWindow(early, None, max_norm)
     late = maxiter if late is None else late
     return CountWindow(early, late, max_norm)

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import assert_iter_count, fixture_window, golden_case, golden_names, rel_l2
+from conftest import assert_fixture_count, golden_case, golden_names, rel_l2
 from oracle import aggregators as orc
 
 pytestmark = pytest.mark.gpu
@@ -81,7 +81,7 @@ def test_panels_match_reference_gm2(name):
     out = bz().gm2(P, o)
     res = bz().aggregators.last_result
     assert rel_l2(out.cpu().numpy(), arr["out"]) <= 1e-5
-    assert_iter_count(res.iters, meta["iters"], fixture_window(name))
+    assert_fixture_count(res.iters, name)
 
 
 def test_panels_store_rows_and_default_guess():
