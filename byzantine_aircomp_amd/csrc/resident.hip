@@ -82,6 +82,15 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 // `sc1` polls are served; an agent-scope (`sc1`) store drops it from the L2, so a
 // same-XCD reader fetches it at the cross-XCD rate (MI355X_MICROARCH.md, store flavours).
 // A granule is one 8-byte store either way (tag and value never torn apart).
+// Hardware contract of the local form (gfx950 only — the library is built for nothing else):
+// the HIP scoped model does not promise that a workgroup-scope store becomes visible to an
+// agent-scope load of another workgroup; here it does because (1) gfx950's vector L1 is
+// write-through, so the `sc0` store reaches the XCD's L2, and (2) the readers' `sc1` polls
+// miss the L1 and read that same L2 — every block of a local grid sits on the one XCD
+// (XCC_ID at the check-in).  tests/test_abi.py test_resident_granule_store_flavours pins the
+// store / poll flavours in the ISA; a break would surface as the 2 s poll timeout, after
+// which the call reruns on the streaming path (single problem) or fails loudly (batched
+// pre-noise begun).
 __device__ __forceinline__ void put_value(gu64* g, unsigned tag, float v, bool local = false) {
   const unsigned long long x = ((unsigned long long)tag << 32) | __float_as_uint(v);
   if (local) __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

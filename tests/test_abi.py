@@ -94,3 +94,43 @@ def test_panel_width_table():
     for K in (1, 16, 17, 100, 256, 257, 600, 1024, 2048):
         W = lib.gm_panel_width(K)
         assert W > 0 and 256 % W == 0          # shard boundaries (256-aligned) stay on panels
+
+
+def _disassemble_bundle(tmp_path, src_index):
+    """The gfx950 code object of the library's `src_index`-th source (Makefile SRCS order),
+    disassembled."""
+    import glob
+    import shutil
+    lib = tmp_path / "lib.so"
+    shutil.copy(_lib.LIB_PATH, lib)
+    subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
+                   capture_output=True, text=True, cwd=tmp_path)
+    co = sorted(glob.glob(str(tmp_path / f"lib.so.{src_index}.hipv4-amdgcn-amd-amdhsa--gfx950")))
+    if not co:
+        pytest.skip("llvm-objdump --offloading unavailable")
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "-d", "--mcpu=gfx950", co[0]],
+                         capture_output=True, text=True, check=True).stdout
+    return out
+
+
+def test_resident_granule_store_flavours(tmp_path):
+    """The single-problem resident kernel's exchange contract (resident.hip put_value /
+    gather_value), pinned in the ISA it was measured on: granules are published with ONE
+    8-byte vector store — `sc0` (workgroup scope: the line stays in the XCD's L2; gfx950's
+    vector L1 is write-through, so the store reaches that L2) when the check-in confirmed
+    one XCD, `sc1` (agent scope) otherwise — and polled with `sc1` vector loads, which miss
+    the L1 and are served by the L2 the writers share.  A compiler that lowered the scoped
+    stores differently would change the measured exchange (and its correctness argument):
+    this fails first, on the CPU."""
+    import re
+    dis = _disassemble_bundle(tmp_path, 2)          # resident.hip (Makefile SRCS order)
+    funcs = re.split(r"\n(?=[0-9a-f]+ <)", dis)
+    res = [f for f in funcs if "weiszfeld_resident" in f.split("\n", 1)[0]]
+    assert res, "no weiszfeld_resident kernel in the resident.hip code object"
+    for f in res:
+        name = f.split("\n", 1)[0]
+        stores = re.findall(r"global_store_dwordx2 [^\n]*", f)
+        assert any(re.search(r"\bsc0\b", s) and not re.search(r"\bsc1\b", s) for s in stores), name
+        assert any(re.search(r"\bsc1\b", s) for s in stores), name
+        polls = re.findall(r"global_load_dwordx2 [^\n]*", f)
+        assert polls and all(re.search(r"\bsc1\b", p) for p in polls), name
