@@ -16,7 +16,7 @@ all: $(LIB)
 
 # gram.hip without SLP vectorization: the f16 Gram producer's per-element FMAs stay
 # scalar v_fma_f32 instead of v_pk_fma_f32, which the MFMA waves sharing its SIMD pay
-# for (C4 shard Gram partial 3.30 -> 2.97 ms; profiles/r2_gram_producer_ab.txt)
+# for (C4 shard Gram partial 3.30 -> 2.97 ms; profiles/history/r2_gram_producer_ab.txt)
 $(BUILD)/gram.o: HIPFLAGS += -fno-slp-vectorize
 
 $(BUILD)/%.o: $(CSRC)/%.hip $(HDRS)

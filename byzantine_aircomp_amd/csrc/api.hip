@@ -113,6 +113,12 @@ int res_xcd_mode() {
   const char* e = getenv("GMAGG_RES_XCD");
   return e ? atoi(e) : 2;
 }
+// GMAGG_RES_HIER (read per call): 1 (default) the XCD-hierarchical gather for resident grids
+// that do not fit one XCD, 0 the flat gather over every block (A/B)
+int res_hier_mode() {
+  const char* e = getenv("GMAGG_RES_HIER");
+  return e ? atoi(e) : 1;
+}
 unsigned res_xcd_stride(int nb, int num_cu) {
   // GMAGG_RES_XCD_BPC=n (A/B): up to n blocks per CU of the one XCD
   static const int bpc = getenv("GMAGG_RES_XCD_BPC") ? std::max(1, atoi(getenv("GMAGG_RES_XCD_BPC"))) : 1;
@@ -284,17 +290,17 @@ bool pick_cfg(int64_t K, int V, int64_t ldx, PassCfg* cfg, bool panel = false) {
   if (K <= 16) { lpr = 64; r = 1; }
   else if (K <= 32) { lpr = 64; r = 2; }
   // 32 < K <= 64 on panels (C5's K = 50 batched problems): 512-thread blocks of 64 x 128
-  // chunks, 5.41-5.49 vs 5.07-5.13 TB/s per C5 STEP pass (profiles/r2_c5_panels.txt); rows
+  // chunks, 5.41-5.49 vs 5.07-5.13 TB/s per C5 STEP pass (profiles/history/r2_c5_panels.txt); rows
   // keep (16,64,4), whose 256-column chunks let C1/C2 stay register-resident
   else if (K <= 64) { if (panel) { nw = 8; lpr = 32; r = 4; } else { lpr = 64; r = 4; } }
   else if (K <= 128) { lpr = 64; r = 8; }
   // 128 < K <= 256 on panels: 256 x 64 chunks (W = 64, each chunk 64 KB contiguous),
   // STEP 2.38 vs 2.54 ms and the C4-shard Gram closing pass 2.58 vs 2.80 ms against the
-  // 256 x 128 tile (profiles/r2_k256_tiles.txt); rows keep the 512-B row segments
+  // 256 x 128 tile (profiles/history/r2_k256_tiles.txt); rows keep the 512-B row segments
   else if (K <= 256) { if (panel) { lpr = 16; r = 4; } else { lpr = 32; r = 8; } }
   else if (K <= 512) { lpr = 16; r = 8; }
   // K <= 1024: two 512-thread blocks per CU, each with a 1024 x 32 tile (128 B row
-  // segments): 6.29 vs 6.05 TB/s for one 1024-thread block (profiles/r01_occ_sweep.txt)
+  // segments): 6.29 vs 6.05 TB/s for one 1024-thread block (profiles/history/r01_occ_sweep.txt)
   else if (K <= 1024) { nw = 8; lpr = 8; r = 16; occ = 2; }
   else if (K <= 2048) { lpr = 4; r = 8; }
   else return false;
@@ -315,7 +321,7 @@ bool pick_cfg(int64_t K, int V, int64_t ldx, PassCfg* cfg, bool panel = false) {
 // Tile of the passes without phase A's weighted sum feeding phase B (INIT) or
 // without phase B (the Gram closing pass): at 128 < K <= 256 the 1-KiB row
 // segments of (16,64,16) beat the STEP tile (16,32,8): 2.81 / 2.76 vs 3.00 /
-// 2.99 ms at K=256 x d=15.6M (profiles/r02_sweep_close.txt).
+// 2.99 ms at K=256 x d=15.6M (profiles/history/r02_sweep_close.txt).
 PassCfg light_cfg(int64_t K, const PassCfg& step) {
   if (getenv("GMAGG_PASS_CFG") || step.V != 4 || K <= 128 || K > 256) return step;
   const PassCfg c{4, 16, 64, 16, 1};
@@ -383,7 +389,11 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   a.checkin = a.gran + (size_t)2 * nb * S;      // (resident_gran_words: + nb + 1 slots)
   a.need = checkin_need((unsigned)nb);
   a.stride = res_xcd_stride(nb, c->num_cu);
-  a.local = a.stride == 8 && res_xcd_mode() == 2;
+  // beyond one XCD: the XCD-hierarchical gather (members -> group leader -> every block),
+  // its member granules L2-kept where the check-in confirms a group on one XCD
+  a.hier = a.stride == 1 && nb > 8 && 2 * K + 2 <= cfg.NW * 64 && res_hier_mode() != 0;
+  a.local = (a.stride == 8 || a.hier) && res_xcd_mode() == 2;
+  a.lvl2 = a.checkin + nb + 1;
   a.bar = bar; a.st = w.st;
   hipEvent_t e0, e1;
   rc = record_pass_begin(c, s, &e0, &e1);
@@ -415,7 +425,9 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   r.last_movement = hst->last_movement;
   r.converged = hst->converged;
   r.algo_used = GM_ALGO_RESIDENT;
-  r.exchange = hbar[0] == 2 ? GM_EXCHANGE_XCD_LOCAL : GM_EXCHANGE_AGENT;   // bar[0] = 1 + local
+  // bar[0] = 1 + local (group 0's, for the hierarchical gather)
+  r.exchange = hbar[0] != 2 ? GM_EXCHANGE_AGENT
+               : a.hier ? GM_EXCHANGE_XCD_HIER : GM_EXCHANGE_XCD_LOCAL;
   if (res) *res = r;
   return GM_OK;
 }
@@ -894,7 +906,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
   const int V = panels ? 4 : pick_vec(X, d, ldx);
   // AUTO: Gram-space (split bf16) for gm2 at K <= 256 on large d, kept if its
   // accuracy guard passes (run_gram); streaming otherwise.  X is read twice
-  // instead of n+1 times (profiles/r01_cmp_algos.txt, r02_gram_split.txt).
+  // instead of n+1 times (profiles/history/r01_cmp_algos.txt, r02_gram_split.txt).
   // Sharded: the choice is made on d_total (every rank the same); each rank's
   // shard must then meet the kernel's local needs, which shard_range-aligned,
   // contiguous shards of a d_total % 4 == 0 update always do.
@@ -1286,7 +1298,7 @@ int gm_weiszfeld_batched_f32(gm_ctx* c, const float* X, int64_t P, int64_t K, in
   // blocks per problem: the grid is OVERSUB rounds of co-resident blocks, so that the
   // iterations where only the slowest problems are still active (the others exit at
   // their `done` flag) still spread over the chip.  C5 on ProblemPanels: 8 rounds
-  // 40.7-41.7k vs 2 rounds 39.7-39.9k problems/s (profiles/r2_c5_oversub.txt;
+  // 40.7-41.7k vs 2 rounds 39.7-39.9k problems/s (profiles/history/r2_c5_oversub.txt;
   // GMAGG_BATCH_OVERSUB: A/B)
   static const int oversub = [] {
     const char* e = getenv("GMAGG_BATCH_OVERSUB");

@@ -1210,7 +1210,7 @@ hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, 
   // GMAGG_SELECT_PERSIST=1: the persistent form (grid-stride tiles, the next tile's loads
   // in registers during the selection).  Measured slower on every shape, so off by default:
   // K=1000 x 2M median 6.14 vs 3.80 ms, trimmed mean 10.5 vs 7.05; K=256 2.07 vs 1.32 and
-  // 4.04 vs 2.52 (two interleaved rounds, profiles/r3s2_select_persist_ab.txt)
+  // 4.04 vs 2.52 (two interleaved rounds, profiles/history/r3s2_select_persist_ab.txt)
   static const int persist = [] {
     const char* e = getenv("GMAGG_SELECT_PERSIST");
     return e ? atoi(e) : 0;

@@ -135,6 +135,13 @@ struct ResArgs {
   // 1: when the check-in finds every block on one XCD, the granules are stored so that
   // they stay in that XCD's L2 (resident.hip put_value); 0: agent-scope stores always
   int local;
+  // XCD-hierarchical gather (grids beyond one XCD, stride 1): blocks b with b % 8 == x form
+  // group x (the blocks dispatch places on XCD x); each block publishes to its group, the
+  // group's first block (the leader) sums its members and publishes the group sum as an
+  // fp32 {hi, lo} granule pair into lvl2 [2][8][2 (2K + 2)]; every block sums the 8 group
+  // sums in group order.  0: the flat gather over every block.
+  int hier;
+  unsigned long long* lvl2;
   KState* st;
 };
 // Plan a resident launch over nch chunks: chunks per block and blocks (false: the

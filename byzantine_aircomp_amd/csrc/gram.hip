@@ -398,7 +398,7 @@ __global__ void __launch_bounds__(512, 1) gram_split_partial(const float* __rest
 // MFMA step and re-issues each committed row's registers for stage s+4 at once
 // (rolling).  One barrier per stage.  The bf16 kernel's two-role block held two
 // sets at most and its producers streamed 5.0 TB/s on their own
-// (profiles/r02_gram_split.txt).  Persistent: one block per CU over a contiguous
+// (profiles/history/r02_gram_split.txt).  Persistent: one block per CU over a contiguous
 // ~d/num_cu column range; the fp32 accumulators are flushed to a partial every
 // kH16Flush stages (8192 columns, the bf16 kernel's accumulation length).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -636,7 +636,7 @@ __device__ __forceinline__ void h16_step(const _Float16* Lh, const _Float16* Lm,
 // 16 x 16, one 32-column k-step per MFMA.  The same cycles per FLOP as 32x32x16; the chip
 // holds a higher clock on the 16x16 shape under load (MI355X_MICROARCH.md 'DVFS
 // give-back' item 7): C4 shard Gram partial 2,976 -> 2,916 us, aggregation 171.3 -> 174.5
-// per s, three interleaved rounds on one box (profiles/r3_gram_shape_ab.jsonl).
+// per s, three interleaved rounds on one box (profiles/history/r3_gram_shape_ab.jsonl).
 // Fragment of rows R0..R0+15, k-step columns c..c+31: lane l holds row R0 + (l & 15),
 // columns c + 8 (l >> 4) .. +7.
 #ifndef GMK_H16_SHAPE

@@ -172,6 +172,43 @@ __device__ __forceinline__ bool gather_value(const gu64* g, int64_t bstride, uns
   return true;
 }
 
+// The XCD-hierarchical gather's second level: value v of the ng group sums, each an fp32
+// {hi, lo} granule pair (hi + lo = the leader's fp64 sum to ~2^-48), polled in one round
+// trip and summed in group order.
+__device__ __forceinline__ bool gather_pairs(const gu64* g, int64_t gstride, unsigned ng,
+                                             unsigned tag, gu32* tmo, double& sum) {
+  unsigned long long hv[8], lv[8];
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if ((unsigned)j < ng) {
+        hv[j] = __hip_atomic_load(g + (int64_t)j * gstride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lv[j] = __hip_atomic_load(g + (int64_t)j * gstride + 1, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+        ok &= (unsigned)(hv[j] >> 32) == tag && (unsigned)(lv[j] >> 32) == tag;
+      }
+    }
+    if (ok) break;
+#if GMK_RES_SLEEP > 0
+    __builtin_amdgcn_s_sleep(GMK_RES_SLEEP);
+#endif
+    if (((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t0 > kPollTicks) ||
+        __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+  sum = 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if ((unsigned)j < ng)
+      sum += (double)__uint_as_float((unsigned)(hv[j] & 0xffffffffull)) +
+             (double)__uint_as_float((unsigned)(lv[j] & 0xffffffffull));
+  return true;
+}
+
 // Granule slots of one block and pass: value v at slot v;
 //   v < K: D2_k; K <= v < 2K: ||x_k||^2 (INIT); 2K, 2K + 1: the block's movement
 //   and ||g||^2 partials (summed over its waves in wave order).
@@ -211,6 +248,16 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   if (blockIdx.x % a.stride) return;                // (stride 8: a placeholder block)
   const unsigned bid = blockIdx.x / a.stride;       // logical block
   const unsigned nb = gridDim.x / a.stride;
+  // XCD-hierarchical gather (a.hier, stride 1): group x = the blocks b % 8 == x, which
+  // round-robin dispatch places on XCD x; the check-in numbers its slots group by group, so
+  // each group's slots are contiguous and its `same` test covers exactly its members
+  const bool hier = a.hier != 0;
+  const unsigned XG = hier ? min(8u, nb) : 1u;
+  const unsigned grp = hier ? bid % 8u : 0u;
+  const unsigned nmem = hier ? (nb - grp + 7u) / 8u : nb;     // blocks of this group
+  const unsigned slot0 = hier ? grp * (nb / 8u) + min(grp, nb % 8u) : 0u;
+  const unsigned slot = hier ? slot0 + bid / 8u : bid;
+  const bool leader = hier && bid < 8u;                      // member 0 of its group
   const int64_t NV = res_values<NW>(K);            // values per block and pass
   const int64_t ch0 = (int64_t)bid * CPB;          // first chunk of this block
   const int64_t gj = ch0 * J + tid;                // finisher column (tid < JB)
@@ -218,10 +265,12 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   gu64* gran = (gu64*)a.gran;                      // [2][nb][2 NV]
   gu32* tmo = (gu32*)a.bar + 2;
   // every block of the grid co-resident before anything is read (device_util.h)
-  if (!grid_checkin(a.checkin, bid, a.need, a.bar + 2, a.bar + 3, kCheckinTicks, &s_ok, &s_same,
-                    0u, nb))
+  if (!grid_checkin(a.checkin, slot, a.need, a.bar + 2, a.bar + 3, kCheckinTicks, &s_ok, &s_same,
+                    slot0, slot0 + nmem))
     return;
-  const bool local = a.local && s_same;            // identical in every block (same slots)
+  // identical in every block of the group (the same slots); hier: the group's member ->
+  // leader granules only (the group sums always go agent-scope)
+  const bool local = a.local && s_same;
   if (bid == 0 && tid == 0)                        // reported to the host (bar[0]: 1 + local)
     __hip_atomic_store((gu32*)a.bar, 1u + (unsigned)local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
@@ -360,7 +409,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
       const unsigned tag = (unsigned)(it + 1);
       const int nk = (int)(it == 0 ? 2 * K : K);
       const int ncol = nk + 2;
-      const int G = max(1, min((int)blockDim.x / ncol, (int)((nb + kNbChunk - 1) / kNbChunk)));
+      const int G = max(1, min((int)blockDim.x / ncol, (int)((nmem + kNbChunk - 1) / kNbChunk)));
       // the K-space step's channel draws do not depend on the data: an idle wave
       // draws them while the others gather
       pre_h2 = a.mode == 1 && K <= 64 && G * ncol <= (NW - 1) * 64;
@@ -384,7 +433,48 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         else s_wp[cc - nk] = sum;
       };
       bool ok = true;
-      if (G == 1) {
+      if (hier) {
+        // level 1, the group's leader: its members' partials (the granules of blocks
+        // grp + 8 m, m < nmem), G thread groups as below, summed in member order
+        if (leader) {
+          if (tid < G * ncol) {
+            const int g = tid / ncol, cc = tid - g * ncol;
+            const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
+            double sum;
+            if (gather_value(in + (int64_t)grp * NV + v, 8 * NV, (unsigned)g, (unsigned)G, nmem,
+                             tag, tmo, sum))
+              s_part[tid] = sum;
+            else
+              ok = false;
+          }
+          if (!ok) s_ok = 0;
+          __syncthreads();
+          if (s_ok == 0) return;
+          gu64* l2o = (gu64*)a.lvl2 + ((int64_t)(it & 1) * 8 + grp) * 2 * NV;
+          for (int cc = tid; cc < ncol; cc += blockDim.x) {
+            double sum = 0.0;
+            for (int g = 0; g < G; ++g) sum += s_part[g * ncol + cc];
+            const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
+            const float hi = (float)sum;
+            put_value(l2o + 2 * v, tag, hi);
+            put_value(l2o + 2 * v + 1, tag, (float)(sum - (double)hi));
+          }
+        }
+        // level 2, every block: the XG group sums in group order (identical everywhere)
+        const gu64* l2i = (const gu64*)a.lvl2 + (int64_t)(it & 1) * 8 * 2 * NV;
+        for (int cc = tid; cc < ncol; cc += blockDim.x) {
+          const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
+          double sum;
+          if (!gather_pairs(l2i + 2 * v, 2 * NV, XG, tag, tmo, sum)) {
+            ok = false;
+            break;
+          }
+          store_value(cc, sum);
+        }
+        if (!ok) s_ok = 0;
+        __syncthreads();
+        if (s_ok == 0) return;
+      } else if (G == 1) {
         for (int cc = tid; cc < ncol; cc += blockDim.x) {
           const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
           double sum;
@@ -503,7 +593,7 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
             }
             // fp32, the reference's own precision (M:403-407): the wave's fp64 divisions
             // and square roots sat on the iteration's critical path; C2 6.38 -> 6.24-6.35 ms
-            // per aggregation (profiles/r2_c2_kspace_fp32.txt)
+            // per aggregation (profiles/history/r2_c2_kspace_fp32.txt)
             const float dist = clamp_dist(s_d2[k], a.eps);
             const float pk = ((float)s_r[k] + s * s) / (dist * dist * (float)(d + 1)) / h2;   // M:404
             const float pup = pk != pk ? pk : fmaxf(pk, thr);          // M:405
@@ -725,8 +815,9 @@ bool resident_plan(const PassCfg& cfg, int64_t nch, int num_cu, int* cpb_out, in
 
 size_t resident_gran_words(int64_t K, const PassCfg& cfg, int nb) {
   (void)cfg;
-  // [2][nb][2K + 2] granules, then nb + 1 co-residency check-in slots
-  return (size_t)2 * nb * (size_t)(2 * K + 2) + (size_t)nb + 1;
+  // [2][nb][2K + 2] granules, then nb + 1 co-residency check-in slots, then the
+  // hierarchical gather's group sums [2][8][2 (2K + 2)]
+  return (size_t)2 * nb * (size_t)(2 * K + 2) + (size_t)nb + 1 + (size_t)32 * (2 * K + 2);
 }
 
 bool res_coop_launch() {
@@ -745,7 +836,7 @@ hipError_t launch_resident(const PassCfg& cfg, int cpb, int grid, const ResArgs&
   // test (and policed by the wall-clock-bounded polls), not by a cooperative launch.  A
   // process that made a cooperative launch segfaults inside the ROCm runtime's exit
   // handlers under rocprofv3 --kernel-trace — a 40-line program with none of this library
-  // does too (tools/coop_exit_probe.hip, profiles/r3s2_c2_exit_crash.txt) — and the plain
+  // does too (tools/coop_exit_probe.hip, profiles/history/r3s2_c2_exit_crash.txt) — and the plain
   // launch costs nothing (C2 158.4 vs 159.7 aggregations/s, interleaved A/B).
   // GMAGG_RES_COOP=1: the cooperative launch (A/B).
   const bool coop = res_coop_launch();

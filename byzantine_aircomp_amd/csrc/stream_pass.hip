@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(NW * 64, OCC * NW / 4) weiszfeld_pass(PassArgs
   // Row r of this thread = wave-uniform row-group base (SGPRs) + ONE 32-bit lane
   // offset shared by all R rows (measured 1.8 % faster than buffer_load with one
   // shared VGPR offset on the C3 pass: 6.90 vs 7.03 ms, same box;
-  // profiles/r02_ab_loads.txt).
+  // profiles/history/r02_ab_loads.txt).
   bool rval[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) rval[i] = rg + (int64_t)NRG * i < K;
@@ -386,13 +386,13 @@ static int pass_variant() {
 
 template <int V, int NW, int LPR, int R, int MODE, int OCC>
 static const void* pass_fn(bool panel) {
-  // Measured on MI355X (profiles/r01_ab_pass.txt, r01_pipe_sweep.txt): the plain
+  // Measured on MI355X (profiles/history/r01_ab_pass.txt, r01_pipe_sweep.txt): the plain
   // pass is as fast or faster than the two-tile PIPE variant at every K, so that
   // one is only built with -DGMK_PIPE_VARIANT for A/B runs.
   // Panels: the rolling-prefetch STEP pass (6.44-6.56 vs 6.63 ms at C3).  INIT stays
   // plain: with the guess on the finisher threads (one load per column instead of
   // one per lane) plain INIT runs at STEP's time, 6.33 vs 6.33 ms, and the rolling
-  // INIT gains nothing, 6.29-6.65 vs STEP 6.32-6.56 (profiles/r2_init_ab.txt).
+  // INIT gains nothing, 6.29-6.65 vs STEP 6.32-6.56 (profiles/history/r2_init_ab.txt).
   constexpr bool kRollDefault = MODE == 0;
   if constexpr (V == 4) {
     if (panel) {
@@ -411,7 +411,7 @@ static const void* pass_fn(bool panel) {
     return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 1, OCC>);
 #endif
   // Row-major STEP passes with float4 rows also take the rolling prefetch: C5's
-  // batched K=50 tile streams 4.64 vs 4.43 TB/s (profiles/r04_c5_roll_ab.txt).
+  // batched K=50 tile streams 4.64 vs 4.43 TB/s (profiles/history/r04_c5_roll_ab.txt).
   if (pass_variant() == 2 || (pass_variant() < 0 && kRollDefault && V == 4))
     return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 2, OCC>);
   return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 0, OCC>);

@@ -129,8 +129,11 @@ enum gm_guard {
 enum gm_exchange {
     GM_EXCHANGE_NONE = 0,      /* launch-per-pass paths: partials reduced between launches */
     GM_EXCHANGE_AGENT = 1,     /* resident grid over several XCDs: agent-scope granule stores */
-    GM_EXCHANGE_XCD_LOCAL = 2  /* resident grid on ONE XCD (confirmed from XCC_ID at the
+    GM_EXCHANGE_XCD_LOCAL = 2, /* resident grid on ONE XCD (confirmed from XCC_ID at the
                                   check-in): granules kept in that XCD's L2 */
+    GM_EXCHANGE_XCD_HIER = 3   /* resident grid over several XCDs, gathered per XCD: each
+                                  block's granules kept in its XCD's L2 for the XCD's leader,
+                                  the 8 per-XCD sums exchanged agent-scope */
 };
 
 typedef struct gm_result {

@@ -2,7 +2,7 @@
 // rocprofv3 --kernel-trace, with none of this library loaded?  (C2's resident kernel
 // is the only cooperative launch of the build; the C2 bench segfaulted inside the HIP
 // runtime's exit handler -> ROCr teardown under rocprofv3, the C3 bench did not:
-// profiles/r3s2_c2_exit_crash.txt.)
+// profiles/history/r3s2_c2_exit_crash.txt.)
 //
 //   hipcc --offload-arch=gfx950 -O2 tools/coop_exit_probe.hip -o tools/coop_exit_probe
 //   rocprofv3 --kernel-trace --stats -d gpurun_out/x -- ./tools/coop_exit_probe [coop|plain]

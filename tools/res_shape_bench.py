@@ -1,7 +1,8 @@
 """Time the single-problem AirComp `gm` (1000 iterations, Philox noise) at several (K, d)
 shapes on the register-resident kernel — the C2 shape and the ones around it (the EMNIST
 MLP's d = 48,670) — so that tile / placement A/Bs (GMAGG_RES_CFG, GMAGG_RES_XCD) can be
-checked beyond C2.  One JSON line per shape:
+checked beyond C2 (GMAGG_RES_HIER: the XCD-hierarchical gather of grids beyond one XCD).
+One JSON line per shape:
 
     python tools/res_shape_bench.py [--shapes 50x7850,50x20000,50x48670] [--reps 5]
 """
@@ -38,7 +39,8 @@ def main():
         ms = (time.perf_counter() - t0) * 1e3 / a.reps
         res = bz.aggregators.last_result
         print(json.dumps({"K": K, "d": d, "ms_per_aggregation": ms, "us_per_iteration": 1e3 * ms / max(res.iters, 1),
-                          "algo": res.algo, "iters": res.iters,
+                          "algo": res.algo, "iters": res.iters, "exchange": res.exchange,
+                          "res_hier": os.environ.get("GMAGG_RES_HIER", "default"),
                           "res_cfg": os.environ.get("GMAGG_RES_CFG", "default"),
                           "res_xcd": os.environ.get("GMAGG_RES_XCD", "default")}), flush=True)
 
