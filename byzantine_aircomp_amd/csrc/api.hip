@@ -113,8 +113,19 @@ int res_xcd_mode() {
   const char* e = getenv("GMAGG_RES_XCD");
   return e ? atoi(e) : 2;
 }
+// GMAGG_RB_HIER=1 (read per call): the batched resident kernel's groups gather by XCD
+// (sub-group leaders, then the <= 3 sub-group sums) instead of flat over the group's 49
+// blocks.  It cuts the C5 AirComp launch's HBM traffic 109.7 -> 33.8 GB (5.3x -> 1.65x the
+// tile read) but measured slower — 818 -> 787 problems/s (AirComp), 70.3k -> 69.1k
+// (prenoise): the exchange is latency-bound, not traffic-bound, and the leader's hop adds
+// latency (profiles/r5s1_c5_rb_hier_ab.jsonl, r5s1_pmc_c5air_hier.txt).  Off by default.
+int rb_hier_mode() {
+  const char* e = getenv("GMAGG_RB_HIER");
+  return e ? atoi(e) : 0;
+}
 // GMAGG_RES_HIER (read per call): 1 (default) the XCD-hierarchical gather for resident grids
-// that do not fit one XCD, 0 the flat gather over every block (A/B)
+// beyond one XCD where it measured faster (>= 150 blocks, K > 32), 2 for every grid beyond
+// one XCD, 0 never (the flat gather over every block)
 int res_hier_mode() {
   const char* e = getenv("GMAGG_RES_HIER");
   return e ? atoi(e) : 1;
@@ -391,7 +402,13 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   a.stride = res_xcd_stride(nb, c->num_cu);
   // beyond one XCD: the XCD-hierarchical gather (members -> group leader -> every block),
   // its member granules L2-kept where the check-in confirms a group on one XCD
-  a.hier = a.stride == 1 && nb > 8 && 2 * K + 2 <= cfg.NW * 64 && res_hier_mode() != 0;
+  // (where it pays, measured: K = 50 × d = 48,670 (191 blocks) 8.45 -> 7.47 µs per iteration,
+  // 50 × 60,000 (235) 8.78 -> 7.38; but 50 × 20,000 (79) 5.99 -> 7.16 and K <= 32 slower at
+  // every size: the leader's extra hop costs more than the polls it saves on smaller grids
+  // or fewer values; profiles/r5s1_resident_hier_shapes_ab.jsonl, r5s1_resident_hier2_ab.jsonl)
+  const int hm = res_hier_mode();
+  a.hier = a.stride == 1 && nb > 8 && 2 * K + 2 <= cfg.NW * 64 &&
+           (hm == 2 || (hm == 1 && nb >= 150 && K > 32));
   a.local = (a.stride == 8 || a.hier) && res_xcd_mode() == 2;
   a.lvl2 = a.checkin + nb + 1;
   a.bar = bar; a.st = w.st;
@@ -499,7 +516,10 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
   a.checkin = reinterpret_cast<unsigned long long*>(b + o_ci);
   a.need = checkin_need(nblocks);
   a.xcd_major = xcd != 0;
-  a.local = xcd == 2;
+  // the hierarchical gather: sub-group granules L2-kept where the check-in confirms them
+  a.hier = xcd != 0 && rb_hier_mode() != 0;
+  a.local = xcd == 2 || a.hier;
+  a.lvl2 = a.gran + (size_t)plan.ng * 2 * plan.nb * (size_t)(2 * K + 2);
   a.st = st;
   hipEvent_t e0, e1;
   rc = record_pass_begin(c, s, &e0, &e1);
@@ -540,8 +560,9 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
     for (int64_t p = 0; p < P; ++p)
       results[p] = gm_result{hst[p].iters, hst[p].last_movement, hst[p].converged,
                              GM_ALGO_RESIDENT, GM_GUARD_NONE, 0,
-                             hflag[1] == (unsigned)plan.ng ? GM_EXCHANGE_XCD_LOCAL
-                                                           : GM_EXCHANGE_AGENT};
+                             a.hier ? GM_EXCHANGE_XCD_HIER
+                             : hflag[1] == (unsigned)plan.ng ? GM_EXCHANGE_XCD_LOCAL
+                                                             : GM_EXCHANGE_AGENT};
   return GM_OK;
 }
 

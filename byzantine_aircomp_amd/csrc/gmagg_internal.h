@@ -182,6 +182,11 @@ struct ResBArgs {
   // 1: groups whose blocks the check-in finds on one XCD store their granules into that
   // XCD's L2 (resident_batched.hip rb_put); the plan then gives each XCD whole groups
   int local;
+  // 1 (with xcd_major): the XCD-hierarchical gather — a group's blocks gather by XCD
+  // (sub-group leaders), then every block sums the <= 8 sub-group sums in lvl2
+  // [NG][2][8][2 (2K + 2)] (resident_batched.hip)
+  int hier;
+  unsigned long long* lvl2;
   KState* st;             // [P]
 };
 struct RbPlan {

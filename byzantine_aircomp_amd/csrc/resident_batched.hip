@@ -117,6 +117,45 @@ __device__ __forceinline__ bool rb_gather(const gu64* g, int64_t bstride, int fi
   return true;
 }
 
+// The hierarchical gather's second level (a.hier): value v of the ns sub-group sums, each
+// an fp32 {hi, lo} granule pair, polled 4 pairs per round trip (the 8 granules of rb_gather's
+// round trip: no more registers beside the tile) and summed in sub-group order.
+__device__ __forceinline__ bool rb_gather_pairs(const gu64* g, int64_t gstride, int ns,
+                                                unsigned tag, gu32* tmo, double& sum) {
+  sum = 0.0;
+  for (int j0 = 0; j0 < ns; j0 += 4) {
+    unsigned long long v[8];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j0 + j < ns) {
+          const gu64* q = g + (int64_t)(j0 + j) * gstride;
+          v[2 * j] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v[2 * j + 1] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok &= (unsigned)(v[2 * j] >> 32) == tag && (unsigned)(v[2 * j + 1] >> 32) == tag;
+        }
+      }
+      if (ok) break;
+#ifndef GMK_RB_NOSLEEP
+      __builtin_amdgcn_s_sleep(GMK_RB_SLEEP);
+#endif
+      if (((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t0 > kRbPollTicks) ||
+          __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j0 + j < ns)
+        sum += (double)__uint_as_float((unsigned)(v[2 * j] & 0xffffffffull)) +
+               (double)__uint_as_float((unsigned)(v[2 * j + 1] & 0xffffffffull));
+  }
+  return true;
+}
+
 // Rows [K0, K0 + R) of a per-thread row quantity (f(k) over the thread's 4 columns),
 // transpose-reduced over the wave: lane c ends with row K0 + row_of_lane<64, R>(c);
 // the lanes c % (64 / R) == 0 hold distinct rows and store them to srow.
@@ -160,7 +199,7 @@ __device__ __forceinline__ void rb_all_rows(F f, float* srow, int lane) {
 // 1 phase B rows, 2 the K-space step, 4 phase A, 8 the
 // gather's wait for the tags, 16 the publish, 32 the tile load, 64 the INIT rows, 128 the
 // LDS rows' loads, 256 the register rows' loads
-template <int KR, int KV, int MODE, int DBG = 0>
+template <int KR, int KV, int MODE, int DBG = 0, bool HIER = false>
 __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   // KR rows per column (K rounded up to 4): rows [0, KV) live in the thread's VGPRs, rows
   // [KV, KR) in LDS (s_x, the thread's own 16 bytes per row).  MODE: gm_mode, a template
@@ -202,9 +241,34 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   }
   const int grp = lb / NB, bi = lb - grp * NB;
   const int NG = (int)gridDim.x / NB;
+  // XCD-hierarchical gather (a.hier, XCD-major numbering): a group's blocks split into
+  // sub-groups by XCD (the group's logical range cut at the XCD ranges: logical blocks
+  // [xlo(x), xlo(x) + n(x)) sit on XCD x); each sub-group's first block (its leader) sums
+  // its members, publishes the sum as an fp32 {hi, lo} pair, and every block sums the
+  // sub-group sums in XCD order.  Without it: one sub-group, the whole group.
+  // (a template parameter: the flat kernels carry none of its registers)
+  const bool hier = HIER && a.xcd_major;
+  auto xcd_lo = [&](int x) {             // first logical block of XCD x (x in 0..8)
+    int b = 0;
+    for (int y = 0; y < x; ++y) b += ((int)gridDim.x - y + 7) >> 3;
+    return b;
+  };
+  int sub_lo = grp * NB, sub_hi = grp * NB + NB, x_first = 0, n_sub = 1, s_idx = 0;
+  if (hier) {
+    const int x = (int)(blockIdx.x & 7);
+    while (x_first < 7 && xcd_lo(x_first + 1) <= grp * NB) ++x_first;
+    int x_last = x_first;
+    while (x_last < 7 && xcd_lo(x_last + 1) < grp * NB + NB) ++x_last;
+    n_sub = x_last - x_first + 1;
+    s_idx = x - x_first;
+    sub_lo = max(grp * NB, xcd_lo(x));
+    sub_hi = min(grp * NB + NB, xcd_lo(x + 1));
+  }
+  const bool leader = hier && lb == sub_lo;
   const int64_t K = a.K, d = a.d;
   const int64_t NV = 2 * K + 2;                    // granule slots per block and pass
   gu64* gran = (gu64*)a.gran + (int64_t)grp * 2 * NB * NV;
+  gu64* lvl2 = (gu64*)a.lvl2 + (int64_t)grp * 2 * 8 * 2 * NV;   // [2][8 sub-groups][2 NV]
   gu32* tmo = (gu32*)a.flag;
   const int64_t W = a.pstride ? ((int64_t)1 << a.wshift) : 0;
   const int64_t rstride = a.pstride ? W : a.ldx;   // between rows k and k + 1
@@ -221,10 +285,11 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   // (slot = logical block: a group's slots are contiguous, so the check-in also tells
   // whether the whole group shares one XCD)
   if (!grid_checkin(a.checkin, (unsigned)lb, a.need, a.flag, a.flag + 2, kCheckinTicks, &s_ok,
-                    &s_same, (unsigned)(grp * NB), (unsigned)(grp * NB + NB)))
+                    &s_same, (unsigned)sub_lo, (unsigned)sub_hi))
     return;
-  const bool local = a.local && s_same;            // identical in the group's blocks
-  if (local && bi == 0 && tid == 0)                // groups on one XCD, counted for the host
+  // identical in the (sub-)group's blocks; hier: the member -> leader granules only
+  const bool local = a.local && s_same;
+  if (local && lb == sub_lo && tid == 0)           // (sub-)groups on one XCD, for the host
     __hip_atomic_fetch_add((gu32*)a.flag + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   f4 x[KV > 0 ? KV : 1];   // the tile's register rows: row k of the thread's 4 columns
@@ -461,8 +526,54 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
       // in group order for the values it needs (no second pass through LDS, no barrier)
       const int nk = (int)((it == 0 && want_r) ? 2 * K : K);
       const int ncol = nk + 2;
-      const int G = max(1, min(NT / ncol, NB));
-      {
+      const int nmem = sub_hi - sub_lo;                // blocks this (sub-)group gathers
+      int G = max(1, min(NT / ncol, nmem));
+      if (hier) {
+        // level 1 (the sub-group's leader) and level 2 (every block): the values land in
+        // s_part[0, ncol) as one "group" for the waves' sums below
+        const gu64* in = gran + (int64_t)(pc & 1) * NB * NV + (int64_t)(sub_lo - grp * NB) * NV;
+        const unsigned tag = pc + 1;
+        bool ok = true;
+        if (leader) {
+          if (tid < G * ncol) {
+            const int gi = tid / ncol, cc = tid - gi * ncol;
+            const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
+            double sum;
+            if (rb_gather(in + v, NV, gi, G, nmem, tag, tmo, sum)) s_part[tid] = sum;
+            else ok = false;
+          }
+          if (!ok) s_ok = 0;
+          __syncthreads();
+          if (s_ok == 0) return;
+          gu64* l2o = lvl2 + ((int64_t)(pc & 1) * 8 + s_idx) * 2 * NV;
+          double sum = 0.0;
+          int64_t v = 0;
+          if (tid < ncol) {
+            for (int gi = 0; gi < G; ++gi) sum += s_part[gi * ncol + tid];
+            v = tid < nk ? tid : 2 * K + (tid - nk);
+          }
+          __syncthreads();                             // (s_part is refilled below)
+          if (tid < ncol) {
+            const float hi = (float)sum;
+            rb_put(l2o + 2 * v, tag, hi, false);
+            rb_put(l2o + 2 * v + 1, tag, (float)(sum - (double)hi), false);
+          }
+        }
+        if (tid < ncol) {
+          const int64_t v = tid < nk ? tid : 2 * K + (tid - nk);
+          double sum;
+          if (rb_gather_pairs(lvl2 + (int64_t)(pc & 1) * 8 * 2 * NV + 2 * v, 2 * NV, n_sub, tag,
+                              tmo, sum))
+            s_part[tid] = sum;
+          else
+            ok = false;
+        }
+        if (!ok) s_ok = 0;
+        __syncthreads();
+        if (s_ok == 0) return;
+        G = 1;
+        ++pc;
+      } else {
         const gu64* in = gran + (int64_t)(pc & 1) * NB * NV;
         const unsigned tag = pc + 1;
         bool ok = true;
@@ -665,7 +776,7 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
 
 // (rows, rows in VGPRs): K <= 32 wholly in registers; K <= 52 with rows 36..51 in LDS
 // (a 52-row register tile does not fit 256 VGPRs beside the kernel's own ~90)
-static const void* rb_kernel(int kr, int mode) {
+static const void* rb_kernel(int kr, int mode, bool hier = false) {
 #ifdef GMK_RB_DBG_VARIANTS
   static const int dbg = getenv("GMAGG_RB_DBG") ? atoi(getenv("GMAGG_RB_DBG")) : 0;
   if (kr == 50 && mode == 0) {
@@ -687,9 +798,12 @@ static const void* rb_kernel(int kr, int mode) {
 #endif
 #define GMK_RB(KR_, KV_, AIRCOMP_)                                                             \
   if (kr == KR_) {                                                                             \
-    if (mode == 0) return reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 0>); \
+    if (mode == 0)                                                                             \
+      return hier ? reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 0, 0, true>) \
+                  : reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 0>);   \
     if constexpr (AIRCOMP_)                                                                    \
-      return reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 1>);          \
+      return hier ? reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 1, 0, true>) \
+                  : reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 1>);   \
     return nullptr;                                                                            \
   }
   // (K <= 50 keeps 32 rows in VGPRs and 18 in LDS (144 KB); K = 51, 52 36 + 16, with a few
@@ -727,11 +841,14 @@ bool rb_plan(int64_t K, int64_t d, int64_t P, int mode, int num_cu, RbPlan* plan
 }
 
 size_t rb_gran_words(int64_t K, const RbPlan& plan) {
-  return (size_t)plan.ng * 2 * plan.nb * (size_t)(2 * K + 2);
+  // [NG][2][NB][2K + 2] granules, then the hierarchical gather's sub-group sums
+  // [NG][2][8][2 (2K + 2)]
+  return (size_t)plan.ng * 2 * plan.nb * (size_t)(2 * K + 2) +
+         (size_t)plan.ng * 32 * (size_t)(2 * K + 2);
 }
 
 hipError_t launch_resident_batched(const RbPlan& plan, const ResBArgs& a, bool coop, hipStream_t s) {
-  const void* fn = rb_kernel(plan.kr, plan.mode);
+  const void* fn = rb_kernel(plan.kr, plan.mode, a.hier != 0);
   if (!fn) return hipErrorInvalidValue;
   void* args[] = {const_cast<ResBArgs*>(&a)};
   const dim3 grid(plan.ng * plan.nb);

@@ -12,6 +12,9 @@ other block across the fabric.
   for gm2, 1e-5 for 200 gm iterations) with the same iteration count;
 * the hierarchical result is reproducible bit for bit (the grouping is fixed by the
   block index, not by where the blocks land).
+
+The parity tests force the hierarchical gather on every grid beyond one XCD
+(GMAGG_RES_HIER=2); AUTO takes it only where it measured faster (test_hier_default_choice).
 """
 import pytest
 import torch
@@ -36,6 +39,7 @@ def _caller(K, d, seed):
 @pytest.mark.parametrize("K,d", SHAPES)
 def test_hier_gm2_vs_oracle_and_flat(K, d, monkeypatch):
     import byzantine_aircomp_amd as bz
+    monkeypatch.setenv("GMAGG_RES_HIER", "2")          # every grid beyond one XCD
     X, p = _caller(K, d, K * 7 + d)
     opts = {"maxiter": 1000, "tol": 1e-5}
     want, tr = orc.gm2(X.clone(), dict(opts, guess=p.clone()))
@@ -59,6 +63,7 @@ def test_hier_gm2_vs_oracle_and_flat(K, d, monkeypatch):
 def test_hier_gm_philox_vs_oracle_and_flat(K, d, monkeypatch):
     import byzantine_aircomp_amd as bz
     from oracle.philox import gm_draws
+    monkeypatch.setenv("GMAGG_RES_HIER", "2")
     X, p = _caller(K, d, K * 11 + d)
     it, seed = 200, 31337
     opts = {"maxiter": it, "tol": 1e-5, "noise_var": 1e-2, "P_max": 1}
@@ -72,6 +77,19 @@ def test_hier_gm_philox_vs_oracle_and_flat(K, d, monkeypatch):
     flat = bz.gm(X.cuda(), dict(opts, guess=p.cuda(), seed=seed))
     assert bz.aggregators.last_result.exchange == "agent"
     assert rel_l2(got.cpu().numpy(), flat.cpu().numpy()) <= 1e-5
+
+
+def test_hier_default_choice():
+    """AUTO takes the hierarchical gather where it measured faster (>= 150 blocks at
+    K > 32: the EMNIST MLP's 50 x 48,670) and the flat gather below (50 x 20,000: 79
+    blocks; K <= 32), profiles/r5s1_resident_hier*_ab.jsonl."""
+    import byzantine_aircomp_amd as bz
+    for (K, d), want in (((50, 48_670), "xcd_hier"), ((50, 20_000), "agent"),
+                         ((10, 48_670), "agent"), ((50, 7850), "xcd_local")):
+        X, p = _caller(K, d, 3)
+        bz.gm2(X.cuda(), {"maxiter": 20, "tol": 1e-5, "guess": p.cuda()})
+        r = bz.aggregators.last_result
+        assert r.algo == "resident" and r.exchange == want, (K, d, r)
 
 
 def test_hier_checkin_failure_streams(monkeypatch):
@@ -103,4 +121,46 @@ def iteration_cases():
     cases = []
     for K, d in SHAPES:
         cases.append((f"hier_{K}x{d}", lambda K=K, d=d: [(*_caller(K, d, K * 7 + d), 1000, 1e-5)]))
+    cases.append(("hier_batched_q5", lambda: [(*_caller(50, 100_000, 905), 1000, 1e-5)]))
     return cases
+
+
+@pytest.mark.parametrize("agg", ["gm2", "gm"])
+def test_batched_hier_vs_flat(agg, monkeypatch):
+    """The batched resident kernel (C5's) with its groups gathering XCD by XCD (sub-group
+    leaders, then the <= 3 sub-group sums; GMAGG_RB_HIER=1, the default) against the flat
+    group gather (GMAGG_RB_HIER=0): the same problems, results equal at the rounding level
+    (gm2: rel L2 <= 1e-6 and the same counts; gm, 300 iterations at var 1e-3 on the caller
+    recipe: <= 1e-5), and problem 5 against the oracle."""
+    import byzantine_aircomp_amd as bz
+    from byzantine_aircomp_amd.batched import SEED_STRIDE, ProblemPanels, gm2_batched, gm_batched
+    from oracle.philox import gm_draws
+    P, K, d = 12, 50, 100_000
+    Xs, ps = zip(*[_caller(K, d, 900 + q) for q in range(P)])
+    X = torch.stack(Xs).cuda()
+    g0 = torch.stack(ps).cuda()
+    Pn = ProblemPanels.from_rows(X)
+    it, seed = 300, 4242
+    opts = {"maxiter": 1000 if agg == "gm2" else it, "tol": 1e-5, "guess": g0}
+    if agg == "gm":
+        opts.update(noise_var=1e-3, seed=seed)
+    run = gm2_batched if agg == "gm2" else gm_batched
+    outs = {}
+    for h in ("1", "0"):
+        monkeypatch.setenv("GMAGG_RB_HIER", h)
+        out, res = run(Pn, dict(opts))
+        assert all(r.algo == "resident" for r in res), res[0]
+        outs[h] = (out.cpu(), res)
+    (a, ra), (b, rb) = outs["1"], outs["0"]
+    assert ra[0].exchange == "xcd_hier" and rb[0].exchange != "xcd_hier"
+    assert [r.iters for r in ra] == [r.iters for r in rb]
+    assert rel_l2(a.numpy(), b.numpy()) <= (1e-6 if agg == "gm2" else 1e-5)
+    q = 5
+    if agg == "gm2":
+        want, tr = orc.gm2(X[q].cpu(), {"maxiter": 1000, "tol": 1e-5, "guess": g0[q].cpu()})
+        assert abs(ra[q].iters - tr.iters) <= 1
+    else:
+        want, tr = orc.gm(X[q].cpu(), {"maxiter": it, "tol": 1e-5, "noise_var": 1e-3, "P_max": 1,
+                                       "guess": g0[q].cpu()},
+                          draw=gm_draws((seed + q * SEED_STRIDE) % 2 ** 64, d))
+    assert rel_l2(a[q].numpy(), want.numpy()) <= 1e-5

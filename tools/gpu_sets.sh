@@ -98,6 +98,36 @@ hier() {
     done
   done
   cat $O/shapes.jsonl
+  # the batched kernel's groups (C5): sub-group gather (GMAGG_RB_HIER=1) against the flat one
+  B="--workload,c5,--no-cpu,--alt-steps,0,--soak,0,--no-check,--steps,1,--warmup,1"
+  timeout -k 10 900 python -u tools/ab.py --rounds 2 --bench=$B --variant hier= --variant flat=GMAGG_RB_HIER=0 \
+    --out $O/ab_c5.jsonl > $O/ab_c5.log 2>&1 || { tail -20 $O/ab_c5.log; return 4; }
+  tail -3 $O/ab_c5.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 2 --bench=$B,--reading,aircomp --variant hier= \
+    --variant flat=GMAGG_RB_HIER=0 --out $O/ab_c5air.jsonl > $O/ab_c5air.log 2>&1 || { tail -20 $O/ab_c5air.log; return 5; }
+  tail -3 $O/ab_c5air.log
+}
+
+hier2() {
+  # Round 5: where the single-problem hierarchical gather starts to pay (grid size x values
+  # per block), and the C5 AirComp launch's HBM traffic with / without the batched one
+  for r in 1 2; do
+    for h in 1 0; do
+      GMAGG_RES_HIER=$h timeout -k 10 200 python -u tools/res_shape_bench.py \
+        --shapes 50x30000,50x40000,50x60000,30x48670,40x48670,20x48670 --reps 5 >> $O/shapes.jsonl || return 3
+    done
+  done
+  cat $O/shapes.jsonl
+  for h in 1 0; do
+    for c in FETCH_SIZE WRITE_SIZE; do
+      GMAGG_RB_HIER=$h timeout -s KILL 400 rocprofv3 --pmc $c --output-format csv -d $O/pmc_h${h}_$c -o p -- \
+        python3 bench.py --workload c5 --reading aircomp --steps 1 --warmup 0 $B_FAST --no-check \
+        > $O/pmc_h${h}_$c.log 2>&1 || return 4
+    done
+    python3 tools/pmc_summary.py $(find $O/pmc_h${h}_FETCH_SIZE -name "*counter_collection.csv" | head -1) \
+      $(find $O/pmc_h${h}_WRITE_SIZE -name "*counter_collection.csv" | head -1) $O/pmc_c5air_h$h.json \
+      "c5air hier=$h" || return 5
+  done
 }
 
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
