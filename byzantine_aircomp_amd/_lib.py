@@ -21,6 +21,7 @@ GM_ALGO_GRAM_F32 = 5
 GM_LAYOUT_ROWS, GM_LAYOUT_PANELS = 0, 1
 GM_GUARD_NONE, GM_GUARD_ACCEPTED, GM_GUARD_REJECTED, GM_GUARD_ACCEPTED_FLOOR = 0, 1, 2, 3
 GM_EXCHANGE_NONE, GM_EXCHANGE_AGENT, GM_EXCHANGE_XCD_LOCAL, GM_EXCHANGE_XCD_HIER = 0, 1, 2, 3
+GM_EXCHANGE_XCD_SPLIT = 4
 
 NOISE_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.POINTER(C.c_float),
                        C.POINTER(C.c_float), C.POINTER(C.c_float))

@@ -59,7 +59,8 @@ class GMResult:
     guard: str = "none"      # Gram guard: "none", "accepted", "accepted_floor", "rejected"
     gram_kind: str = ""      # Gram runs: "f16_split", "bf16_split" (f16 range fallback), "f32"
     exchange: str = "none"   # resident runs: "agent" (flat, over XCDs), "xcd_local" (one XCD's
-    #                          L2) or "xcd_hier" (per-XCD gather, then the 8 XCD sums)
+    #                          L2), "xcd_hier" (per-XCD gather, then the 8 XCD sums) or
+    #                          "xcd_split" (one hop, own-XCD blocks from L2-kept copies)
 
 
 last_result: GMResult | None = None
@@ -75,7 +76,8 @@ def _result(res) -> "GMResult":
     return GMResult(res.iters, res.last_movement, bool(res.converged),
                     _ALGO_NAMES.get(res.algo_used, "?"), _GUARD_NAMES.get(res.guard, "?"),
                     {1: "f16_split", 2: "bf16_split", 3: "f32"}.get(res.gram_kind, ""),
-                    {1: "agent", 2: "xcd_local", 3: "xcd_hier"}.get(res.exchange, "none"))
+                    {1: "agent", 2: "xcd_local", 3: "xcd_hier",
+                     4: "xcd_split"}.get(res.exchange, "none"))
 
 
 class Context:

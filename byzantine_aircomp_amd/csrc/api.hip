@@ -123,8 +123,16 @@ int rb_hier_mode() {
   const char* e = getenv("GMAGG_RB_HIER");
   return e ? atoi(e) : 0;
 }
+// GMAGG_RES_SPLIT (read per call): 1 (default) the split-scope exchange for resident grids
+// beyond one XCD that do not take the hierarchical gather (results bit-identical to the
+// flat gather's; 50 x 20,000 6.03 -> 5.95 µs per iteration, 50 x 30,000 6.75 -> 6.62,
+// 30 x 48,670 6.95 -> 6.77; profiles/r5s1_resident_split_ab.jsonl), 0 the flat gather
+int res_split_mode() {
+  const char* e = getenv("GMAGG_RES_SPLIT");
+  return e ? atoi(e) : 1;
+}
 // GMAGG_RES_HIER (read per call): 1 (default) the XCD-hierarchical gather for resident grids
-// beyond one XCD where it measured faster (>= 150 blocks, K > 32), 2 for every grid beyond
+// beyond one XCD where it measured faster (>= 90 blocks, K > 32), 2 for every grid beyond
 // one XCD, 0 never (the flat gather over every block)
 int res_hier_mode() {
   const char* e = getenv("GMAGG_RES_HIER");
@@ -402,15 +410,20 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   a.stride = res_xcd_stride(nb, c->num_cu);
   // beyond one XCD: the XCD-hierarchical gather (members -> group leader -> every block),
   // its member granules L2-kept where the check-in confirms a group on one XCD
-  // (where it pays, measured: K = 50 × d = 48,670 (191 blocks) 8.45 -> 7.47 µs per iteration,
-  // 50 × 60,000 (235) 8.78 -> 7.38; but 50 × 20,000 (79) 5.99 -> 7.16 and K <= 32 slower at
-  // every size: the leader's extra hop costs more than the polls it saves on smaller grids
-  // or fewer values; profiles/r5s1_resident_hier_shapes_ab.jsonl, r5s1_resident_hier2_ab.jsonl)
+  // (where it pays, measured: K = 50 × d = 48,670 (96 blocks of 512 columns) 8.45 -> 7.47 µs
+  // per iteration, 50 × 60,000 (118 blocks) 8.78 -> 7.38; but 50 × 30,000 (59) 6.72 -> 7.32,
+  // 50 × 20,000 (40) 5.99 -> 7.16 and K <= 32 slower at every size: the leader's extra hop
+  // costs more than the polls it saves on smaller grids or fewer values;
+  // profiles/r5s1_resident_hier_shapes_ab.jsonl, r5s1_resident_hier2_ab.jsonl)
   const int hm = res_hier_mode();
   a.hier = a.stride == 1 && nb > 8 && 2 * K + 2 <= cfg.NW * 64 &&
-           (hm == 2 || (hm == 1 && nb >= 150 && K > 32));
+           (hm == 2 || (hm == 1 && nb >= 90 && K > 32));
   a.local = (a.stride == 8 || a.hier) && res_xcd_mode() == 2;
   a.lvl2 = a.checkin + nb + 1;
+  // below the hierarchical gather's range: the split-scope exchange (one hop, as the flat
+  // gather, but each reader polls its own XCD's blocks from L2-kept copies)
+  a.split = a.stride == 1 && !a.hier && nb > 8 && res_xcd_mode() == 2 && res_split_mode() != 0;
+  a.granL = a.lvl2 + (size_t)32 * (2 * K + 2);
   a.bar = bar; a.st = w.st;
   hipEvent_t e0, e1;
   rc = record_pass_begin(c, s, &e0, &e1);
@@ -444,7 +457,8 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   r.algo_used = GM_ALGO_RESIDENT;
   // bar[0] = 1 + local (group 0's, for the hierarchical gather)
   r.exchange = hbar[0] != 2 ? GM_EXCHANGE_AGENT
-               : a.hier ? GM_EXCHANGE_XCD_HIER : GM_EXCHANGE_XCD_LOCAL;
+               : a.hier ? GM_EXCHANGE_XCD_HIER
+               : a.split ? GM_EXCHANGE_XCD_SPLIT : GM_EXCHANGE_XCD_LOCAL;
   if (res) *res = r;
   return GM_OK;
 }
@@ -517,8 +531,8 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
   a.need = checkin_need(nblocks);
   a.xcd_major = xcd != 0;
   // the hierarchical gather: sub-group granules L2-kept where the check-in confirms them
-  a.hier = xcd != 0 && rb_hier_mode() != 0;
-  a.local = xcd == 2 || a.hier;
+  a.hier = xcd != 0 && rb_hier_mode() == 1;
+  a.local = xcd == 2 || a.hier != 0;
   a.lvl2 = a.gran + (size_t)plan.ng * 2 * plan.nb * (size_t)(2 * K + 2);
   a.st = st;
   hipEvent_t e0, e1;
@@ -560,7 +574,7 @@ int run_resident_batched(gm_ctx* c, const float* X, int64_t P, int64_t K, int64_
     for (int64_t p = 0; p < P; ++p)
       results[p] = gm_result{hst[p].iters, hst[p].last_movement, hst[p].converged,
                              GM_ALGO_RESIDENT, GM_GUARD_NONE, 0,
-                             a.hier ? GM_EXCHANGE_XCD_HIER
+                             a.hier == 1 ? GM_EXCHANGE_XCD_HIER
                              : hflag[1] == (unsigned)plan.ng ? GM_EXCHANGE_XCD_LOCAL
                                                              : GM_EXCHANGE_AGENT};
   return GM_OK;

@@ -142,6 +142,11 @@ struct ResArgs {
   // sums in group order.  0: the flat gather over every block.
   int hier;
   unsigned long long* lvl2;
+  // split-scope exchange (stride 1, not hier): every granule also stored L2-kept into
+  // granL [2][gridDim.x][2K + 2]; a reader polls its own XCD's blocks (b % 8 == its group)
+  // there once the check-in confirms the group on one XCD
+  int split;
+  unsigned long long* granL;
   KState* st;
 };
 // Plan a resident launch over nch chunks: chunks per block and blocks (false: the

@@ -172,6 +172,46 @@ __device__ __forceinline__ bool gather_value(const gu64* g, int64_t bstride, uns
   return true;
 }
 
+// The split-scope exchange (a.split): gather_value over blocks whose granules sit in one of
+// two copies — blocks b % 8 == mine (the reader's own XCD) from the L2-kept copy gL, every
+// other block from the agent-scope copy g.  The same values in the same order: the same sum.
+__device__ __forceinline__ bool gather_value_split(const gu64* g, const gu64* gL, int64_t bstride,
+                                                   unsigned b_first, unsigned b_step, unsigned nb,
+                                                   unsigned mine, unsigned tag, gu32* tmo,
+                                                   double& sum) {
+  sum = 0.0;
+  for (unsigned b0 = b_first; b0 < nb; b0 += kNbChunk * b_step) {
+    unsigned long long hi[kNbChunk];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j < kNbChunk; ++j) {
+        const unsigned b = b0 + j * b_step;
+        if (b < nb) {
+          const gu64* q = ((b & 7u) == mine ? gL : g) + (int64_t)b * bstride;
+          hi[j] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok &= (unsigned)(hi[j] >> 32) == tag;
+        }
+      }
+      if (ok) break;
+#if GMK_RES_SLEEP > 0
+      __builtin_amdgcn_s_sleep(GMK_RES_SLEEP);
+#endif
+      if (((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t0 > kPollTicks) ||
+          __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kNbChunk; ++j)
+      if (b0 + j * b_step < nb)
+        sum += (double)__uint_as_float((unsigned)(hi[j] & 0xffffffffull));
+  }
+  return true;
+}
+
 // The XCD-hierarchical gather's second level: value v of the ng group sums, each an fp32
 // {hi, lo} granule pair (hi + lo = the leader's fp64 sum to ~2^-48), polled in one round
 // trip and summed in group order.
@@ -252,11 +292,17 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   // round-robin dispatch places on XCD x; the check-in numbers its slots group by group, so
   // each group's slots are contiguous and its `same` test covers exactly its members
   const bool hier = a.hier != 0;
+  // split scope (a.split, stride 1, not hier): one hop as the flat gather, each granule
+  // published agent-scope AND L2-kept; a reader polls the L2-kept copies of its own group
+  // (XCD) once the check-in confirms the group on one XCD
+  const bool split = a.split != 0 && !hier;
+  const bool xg = hier || split;
   const unsigned XG = hier ? min(8u, nb) : 1u;
-  const unsigned grp = hier ? bid % 8u : 0u;
-  const unsigned nmem = hier ? (nb - grp + 7u) / 8u : nb;     // blocks of this group
-  const unsigned slot0 = hier ? grp * (nb / 8u) + min(grp, nb % 8u) : 0u;
-  const unsigned slot = hier ? slot0 + bid / 8u : bid;
+  const unsigned grp = xg ? bid % 8u : 0u;
+  const unsigned nmem = hier ? (nb - grp + 7u) / 8u : nb;     // blocks this block gathers
+  const unsigned ngrp = xg ? (nb - grp + 7u) / 8u : nb;       // blocks of this group
+  const unsigned slot0 = xg ? grp * (nb / 8u) + min(grp, nb % 8u) : 0u;
+  const unsigned slot = xg ? slot0 + bid / 8u : bid;
   const bool leader = hier && bid < 8u;                      // member 0 of its group
   const int64_t NV = res_values<NW>(K);            // values per block and pass
   const int64_t ch0 = (int64_t)bid * CPB;          // first chunk of this block
@@ -266,13 +312,16 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   gu32* tmo = (gu32*)a.bar + 2;
   // every block of the grid co-resident before anything is read (device_util.h)
   if (!grid_checkin(a.checkin, slot, a.need, a.bar + 2, a.bar + 3, kCheckinTicks, &s_ok, &s_same,
-                    slot0, slot0 + nmem))
+                    slot0, slot0 + ngrp))
     return;
   // identical in every block of the group (the same slots); hier: the group's member ->
   // leader granules only (the group sums always go agent-scope)
-  const bool local = a.local && s_same;
+  const bool local = a.local && s_same && !split;
+  const unsigned mine = (split && s_same) ? grp : 8u;        // split: the group read from gL
+  gu64* granL = (gu64*)a.granL;                              // split: [2][nb][NV] L2-kept copies
   if (bid == 0 && tid == 0)                        // reported to the host (bar[0]: 1 + local)
-    __hip_atomic_store((gu32*)a.bar, 1u + (unsigned)local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32*)a.bar, 1u + (unsigned)(local || mine < 8u), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 
   // ---- the block's tiles: loaded once, resident for the whole call
   float x[CPB][R][V];
@@ -312,14 +361,19 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   // publish this block's partials of pass p (granules, tag p + 1, buffer p & 1)
   auto publish = [&](int64_t p, const double* racc, const double* racc2, double mv, double gn) {
     gu64* out = gran + ((p & 1) * nb + bid) * NV;
+    gu64* outL = granL + ((p & 1) * nb + bid) * NV;
     const unsigned tag = (unsigned)(p + 1);
+    auto put = [&](int64_t slot, float v) {
+      put_value(out + slot, tag, v, local);
+      if (split) put_value(outL + slot, tag, v, true);
+    };
     if ((c % SPAN) == 0) {
 #pragma unroll
       for (int m = 0; m < RPL; ++m) {
         const int64_t k = rg + (int64_t)NRG * (i_c + m);
         if (k < K) {
-          put_value(out + k, tag, (float)racc[m], local);
-          if (racc2) put_value(out + K + k, tag, (float)racc2[m], local);
+          put(k, (float)racc[m]);
+          if (racc2) put(K + k, (float)racc2[m]);
         }
       }
     }
@@ -329,8 +383,8 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         m += s_fin[0][ww];
         g += s_fin[1][ww];
       }
-      put_value(out + 2 * K, tag, (float)m, local);
-      put_value(out + 2 * K + 1, tag, (float)g, local);
+      put(2 * K, (float)m);
+      put(2 * K + 1, (float)g);
     }
   };
   // wave partials of the movement and ||g||^2 -> s_fin (read by publish after a
@@ -478,7 +532,9 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
         for (int cc = tid; cc < ncol; cc += blockDim.x) {
           const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
           double sum;
-          if (!gather_value(in + v, NV, 0u, 1u, nb, tag, tmo, sum)) {
+          const gu64* inL = granL + (it & 1) * nb * NV;
+          if (!(split ? gather_value_split(in + v, inL + v, NV, 0u, 1u, nb, mine, tag, tmo, sum)
+                      : gather_value(in + v, NV, 0u, 1u, nb, tag, tmo, sum))) {
             ok = false;
             break;
           }
@@ -492,8 +548,13 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
           const int g = tid / ncol, cc = tid - g * ncol;
           const int64_t v = cc < nk ? cc : 2 * K + (cc - nk);
           double sum;
-          if (gather_value(in + v, NV, (unsigned)g, (unsigned)G, nb, tag, tmo, sum)) s_part[tid] = sum;
-          else ok = false;
+          const gu64* inL = granL + (it & 1) * nb * NV;
+          if (split ? gather_value_split(in + v, inL + v, NV, (unsigned)g, (unsigned)G, nb, mine,
+                                         tag, tmo, sum)
+                    : gather_value(in + v, NV, (unsigned)g, (unsigned)G, nb, tag, tmo, sum))
+            s_part[tid] = sum;
+          else
+            ok = false;
         }
         if (!ok) s_ok = 0;
         __syncthreads();
@@ -816,8 +877,9 @@ bool resident_plan(const PassCfg& cfg, int64_t nch, int num_cu, int* cpb_out, in
 size_t resident_gran_words(int64_t K, const PassCfg& cfg, int nb) {
   (void)cfg;
   // [2][nb][2K + 2] granules, then nb + 1 co-residency check-in slots, then the
-  // hierarchical gather's group sums [2][8][2 (2K + 2)]
-  return (size_t)2 * nb * (size_t)(2 * K + 2) + (size_t)nb + 1 + (size_t)32 * (2 * K + 2);
+  // hierarchical gather's group sums [2][8][2 (2K + 2)], then the split-scope exchange's
+  // L2-kept copies [2][nb][2K + 2]
+  return (size_t)4 * nb * (size_t)(2 * K + 2) + (size_t)nb + 1 + (size_t)32 * (2 * K + 2);
 }
 
 bool res_coop_launch() {

@@ -199,7 +199,7 @@ __device__ __forceinline__ void rb_all_rows(F f, float* srow, int lane) {
 // 1 phase B rows, 2 the K-space step, 4 phase A, 8 the
 // gather's wait for the tags, 16 the publish, 32 the tile load, 64 the INIT rows, 128 the
 // LDS rows' loads, 256 the register rows' loads
-template <int KR, int KV, int MODE, int DBG = 0, bool HIER = false>
+template <int KR, int KV, int MODE, int DBG = 0, int XG = 0>
 __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   // KR rows per column (K rounded up to 4): rows [0, KV) live in the thread's VGPRs, rows
   // [KV, KR) in LDS (s_x, the thread's own 16 bytes per row).  MODE: gm_mode, a template
@@ -246,8 +246,11 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   // [xlo(x), xlo(x) + n(x)) sit on XCD x); each sub-group's first block (its leader) sums
   // its members, publishes the sum as an fp32 {hi, lo} pair, and every block sums the
   // sub-group sums in XCD order.  Without it: one sub-group, the whole group.
-  // (a template parameter: the flat kernels carry none of its registers)
-  const bool hier = HIER && a.xcd_major;
+  // XG (a template parameter: the flat kernels carry none of its registers): 0 flat, 1 the
+  // sub-group leaders above.  (A split-scope variant — every granule published agent-scope
+  // and L2-kept, each reader polling its own XCD's blocks from the L2-kept copy: one hop —
+  // measured slower still, C5 AirComp 815 -> 736 problems/s; profiles/r5s1_c5_rb_split_ab.jsonl)
+  const bool hier = XG == 1 && a.xcd_major;
   auto xcd_lo = [&](int x) {             // first logical block of XCD x (x in 0..8)
     int b = 0;
     for (int y = 0; y < x; ++y) b += ((int)gridDim.x - y + 7) >> 3;
@@ -310,19 +313,20 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
   auto publish = [&](bool with_r) {
     gu64* out = gran + ((int64_t)(pc & 1) * NB + bi) * NV;
     const unsigned tag = pc + 1;
+    auto put = [&](int64_t slot, float v) { rb_put(out + slot, tag, v, local); };
     const int pb = pc & 1;
     if (tid < K) {
       double sm = 0.0;
 #pragma unroll
       for (int ww = 0; ww < NW; ++ww) sm += (double)s_rows[pb][ww][tid];
-      rb_put(out + tid, tag, (float)sm, local);
+      put(tid, (float)sm);
     }
     if (with_r && tid >= 64 && tid < 64 + K) {
       const int k = tid - 64;
       double sm = 0.0;
 #pragma unroll
       for (int ww = 0; ww < NW; ++ww) sm += (double)s_rows2[ww][k];
-      rb_put(out + K + k, tag, (float)sm, local);
+      put(K + k, (float)sm);
     }
     if (tid == 128) {
       double m = 0.0, gg = 0.0;
@@ -331,8 +335,8 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
         m += (double)s_fin[pb][0][ww];
         gg += (double)s_fin[pb][1][ww];
       }
-      rb_put(out + 2 * K, tag, (float)m, local);
-      rb_put(out + 2 * K + 1, tag, (float)gg, local);
+      put(2 * K, (float)m);
+      put(2 * K + 1, (float)gg);
     }
   };
   auto wave_fin = [&](float mv, float gn) {
@@ -776,7 +780,7 @@ __global__ void __launch_bounds__(512) weiszfeld_resident_batched(ResBArgs a) {
 
 // (rows, rows in VGPRs): K <= 32 wholly in registers; K <= 52 with rows 36..51 in LDS
 // (a 52-row register tile does not fit 256 VGPRs beside the kernel's own ~90)
-static const void* rb_kernel(int kr, int mode, bool hier = false) {
+static const void* rb_kernel(int kr, int mode, int xg = 0) {
 #ifdef GMK_RB_DBG_VARIANTS
   static const int dbg = getenv("GMAGG_RB_DBG") ? atoi(getenv("GMAGG_RB_DBG")) : 0;
   if (kr == 50 && mode == 0) {
@@ -796,14 +800,13 @@ static const void* rb_kernel(int kr, int mode, bool hier = false) {
     }
   }
 #endif
+#define GMK_RB_XG(KR_, KV_, M_)                                                                \
+  (xg == 1 ? reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, M_, 0, 1>)    \
+           : reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, M_>))
 #define GMK_RB(KR_, KV_, AIRCOMP_)                                                             \
   if (kr == KR_) {                                                                             \
-    if (mode == 0)                                                                             \
-      return hier ? reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 0, 0, true>) \
-                  : reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 0>);   \
-    if constexpr (AIRCOMP_)                                                                    \
-      return hier ? reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 1, 0, true>) \
-                  : reinterpret_cast<const void*>(&weiszfeld_resident_batched<KR_, KV_, 1>);   \
+    if (mode == 0) return GMK_RB_XG(KR_, KV_, 0);                                              \
+    if constexpr (AIRCOMP_) return GMK_RB_XG(KR_, KV_, 1);                                     \
     return nullptr;                                                                            \
   }
   // (K <= 50 keeps 32 rows in VGPRs and 18 in LDS (144 KB); K = 51, 52 36 + 16, with a few
@@ -811,6 +814,7 @@ static const void* rb_kernel(int kr, int mode, bool hier = false) {
   // loop invariants, ~44 scratch reloads per iteration)
   GMK_RB(16, 16, true) GMK_RB(32, 32, true) GMK_RB(50, 32, true) GMK_RB(52, 36, false)
 #undef GMK_RB
+#undef GMK_RB_XG
   return nullptr;
 }
 
@@ -848,7 +852,7 @@ size_t rb_gran_words(int64_t K, const RbPlan& plan) {
 }
 
 hipError_t launch_resident_batched(const RbPlan& plan, const ResBArgs& a, bool coop, hipStream_t s) {
-  const void* fn = rb_kernel(plan.kr, plan.mode, a.hier != 0);
+  const void* fn = rb_kernel(plan.kr, plan.mode, a.hier);
   if (!fn) return hipErrorInvalidValue;
   void* args[] = {const_cast<ResBArgs*>(&a)};
   const dim3 grid(plan.ng * plan.nb);

@@ -131,9 +131,12 @@ enum gm_exchange {
     GM_EXCHANGE_AGENT = 1,     /* resident grid over several XCDs: agent-scope granule stores */
     GM_EXCHANGE_XCD_LOCAL = 2, /* resident grid on ONE XCD (confirmed from XCC_ID at the
                                   check-in): granules kept in that XCD's L2 */
-    GM_EXCHANGE_XCD_HIER = 3   /* resident grid over several XCDs, gathered per XCD: each
+    GM_EXCHANGE_XCD_HIER = 3,  /* resident grid over several XCDs, gathered per XCD: each
                                   block's granules kept in its XCD's L2 for the XCD's leader,
                                   the 8 per-XCD sums exchanged agent-scope */
+    GM_EXCHANGE_XCD_SPLIT = 4  /* resident grid over several XCDs, one hop: each granule stored
+                                  agent-scope and L2-kept, a reader polling its own XCD's
+                                  blocks from the L2-kept copies */
 };
 
 typedef struct gm_result {

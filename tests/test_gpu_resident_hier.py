@@ -1,5 +1,5 @@
 """The single-problem register-resident kernel on grids larger than one XCD (round 5,
-VERDICT r4 item 6): the EMNIST MLP (E:101, d = 48,670: 191 blocks) and 50 x 20,000 (79
+VERDICT r4 item 6): the EMNIST MLP (E:101, d = 48,670: 96 blocks) and 50 x 20,000 (40
 blocks) gather XCD by XCD — each block's partials L2-kept for its XCD's leader, the 8 per-XCD
 sums exchanged agent-scope (resident.hip, `a.hier`) — instead of every block polling every
 other block across the fabric.
@@ -52,6 +52,7 @@ def test_hier_gm2_vs_oracle_and_flat(K, d, monkeypatch):
     b = bz.gm2(Xd, dict(opts, guess=pd))
     assert torch.equal(a, b)                               # reproducible
     monkeypatch.setenv("GMAGG_RES_HIER", "0")
+    monkeypatch.setenv("GMAGG_RES_SPLIT", "0")          # the flat gather
     f = bz.gm2(Xd, dict(opts, guess=pd))
     rf = bz.aggregators.last_result
     assert rf.algo == "resident" and rf.exchange == "agent", rf
@@ -74,18 +75,40 @@ def test_hier_gm_philox_vs_oracle_and_flat(K, d, monkeypatch):
     assert tr.iters == it
     assert rel_l2(got.cpu().numpy(), ref.numpy()) <= 1e-5
     monkeypatch.setenv("GMAGG_RES_HIER", "0")
+    monkeypatch.setenv("GMAGG_RES_SPLIT", "0")          # the flat gather
     flat = bz.gm(X.cuda(), dict(opts, guess=p.cuda(), seed=seed))
     assert bz.aggregators.last_result.exchange == "agent"
     assert rel_l2(got.cpu().numpy(), flat.cpu().numpy()) <= 1e-5
 
 
-def test_hier_default_choice():
-    """AUTO takes the hierarchical gather where it measured faster (>= 150 blocks at
-    K > 32: the EMNIST MLP's 50 x 48,670) and the flat gather below (50 x 20,000: 79
-    blocks; K <= 32), profiles/r5s1_resident_hier*_ab.jsonl."""
+@pytest.mark.parametrize("K,d", [(50, 20_000), (10, 48_670)])
+def test_split_scope_equals_flat(K, d, monkeypatch):
+    """The split-scope exchange (GMAGG_RES_SPLIT=1: every granule published agent-scope and
+    L2-kept, each reader polling its own XCD's blocks from the L2-kept copy) carries the
+    same values in the same order as the flat gather: bit-identical results, gm2 and gm."""
     import byzantine_aircomp_amd as bz
-    for (K, d), want in (((50, 48_670), "xcd_hier"), ((50, 20_000), "agent"),
-                         ((10, 48_670), "agent"), ((50, 7850), "xcd_local")):
+    X, p = _caller(K, d, 77)
+    Xd, pd = X.cuda(), p.cuda()
+    for agg, opts in (("gm2", {"maxiter": 1000, "tol": 1e-5}),
+                      ("gm", {"maxiter": 100, "tol": 1e-5, "noise_var": 1e-4, "seed": 3})):
+        outs = {}
+        for sp in ("1", "0"):
+            monkeypatch.setenv("GMAGG_RES_SPLIT", sp)
+            outs[sp] = (getattr(bz, agg)(Xd, dict(opts, guess=pd)), bz.aggregators.last_result)
+        (a, ra), (b, rb) = outs["1"], outs["0"]
+        assert ra.algo == rb.algo == "resident" and ra.iters == rb.iters, (ra, rb)
+        assert (ra.exchange, rb.exchange) == ("xcd_split", "agent"), (ra, rb)
+        assert bool(torch.isfinite(a).all()) and torch.equal(a, b)
+
+
+def test_hier_default_choice():
+    """AUTO takes the hierarchical gather where it measured faster (>= 90 blocks at
+    K > 32: the EMNIST MLP's 50 x 48,670, 96 blocks) and the split-scope one-hop exchange on
+    the other grids beyond one XCD (50 x 20,000: 40 blocks; K <= 32),
+    profiles/r5s1_resident_*_ab.jsonl."""
+    import byzantine_aircomp_amd as bz
+    for (K, d), want in (((50, 48_670), "xcd_hier"), ((50, 20_000), "xcd_split"),
+                         ((10, 48_670), "xcd_split"), ((50, 7850), "xcd_local")):
         X, p = _caller(K, d, 3)
         bz.gm2(X.cuda(), {"maxiter": 20, "tol": 1e-5, "guess": p.cuda()})
         r = bz.aggregators.last_result
@@ -125,11 +148,13 @@ def iteration_cases():
     return cases
 
 
+@pytest.mark.parametrize("mode", ["1"])
 @pytest.mark.parametrize("agg", ["gm2", "gm"])
-def test_batched_hier_vs_flat(agg, monkeypatch):
-    """The batched resident kernel (C5's) with its groups gathering XCD by XCD (sub-group
-    leaders, then the <= 3 sub-group sums; GMAGG_RB_HIER=1, the default) against the flat
-    group gather (GMAGG_RB_HIER=0): the same problems, results equal at the rounding level
+def test_batched_hier_vs_flat(agg, mode, monkeypatch):
+    """The batched resident kernel (C5's) with its groups gathering XCD by XCD (mode 1:
+    sub-group leaders, then the <= 3 sub-group sums; an A/B knob, off by default) against
+    the flat group gather (GMAGG_RB_HIER=0, the default): the same problems, results equal
+    at the rounding level
     (gm2: rel L2 <= 1e-6 and the same counts; gm, 300 iterations at var 1e-3 on the caller
     recipe: <= 1e-5), and problem 5 against the oracle."""
     import byzantine_aircomp_amd as bz
@@ -146,14 +171,16 @@ def test_batched_hier_vs_flat(agg, monkeypatch):
         opts.update(noise_var=1e-3, seed=seed)
     run = gm2_batched if agg == "gm2" else gm_batched
     outs = {}
-    for h in ("1", "0"):
+    for h in (mode, "0"):
         monkeypatch.setenv("GMAGG_RB_HIER", h)
         out, res = run(Pn, dict(opts))
         assert all(r.algo == "resident" for r in res), res[0]
         outs[h] = (out.cpu(), res)
-    (a, ra), (b, rb) = outs["1"], outs["0"]
-    assert ra[0].exchange == "xcd_hier" and rb[0].exchange != "xcd_hier"
+    (a, ra), (b, rb) = outs[mode], outs["0"]
+    assert (ra[0].exchange == "xcd_hier") == (mode == "1") and rb[0].exchange != "xcd_hier"
     assert [r.iters for r in ra] == [r.iters for r in rb]
+    if mode == "2":
+        assert torch.equal(a, b)
     assert rel_l2(a.numpy(), b.numpy()) <= (1e-6 if agg == "gm2" else 1e-5)
     q = 5
     if agg == "gm2":

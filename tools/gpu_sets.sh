@@ -130,6 +130,39 @@ hier2() {
   done
 }
 
+split() {
+  # Round 5: the batched kernel's split-scope exchange (GMAGG_RB_HIER=2: one hop, each
+  # granule agent-scope + L2-kept, read from its XCD's copy) against the flat one: parity,
+  # C5 A/B (both readings), the AirComp launch's HBM traffic
+  timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+    tests/test_gpu_resident_hier.py -k batched > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  B="--workload,c5,--no-cpu,--alt-steps,0,--soak,0,--no-check,--steps,1,--warmup,1"
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=$B,--reading,aircomp --variant split=GMAGG_RB_HIER=2 \
+    --variant flat= --out $O/ab_c5air.jsonl > $O/ab_c5air.log 2>&1 || { tail -20 $O/ab_c5air.log; return 5; }
+  tail -2 $O/ab_c5air.log
+  timeout -k 10 900 python -u tools/ab.py --rounds 2 --bench=$B --variant split=GMAGG_RB_HIER=2 --variant flat= \
+    --out $O/ab_c5.jsonl > $O/ab_c5.log 2>&1 || { tail -20 $O/ab_c5.log; return 4; }
+  tail -2 $O/ab_c5.log
+  for c in FETCH_SIZE WRITE_SIZE; do
+    GMAGG_RB_HIER=2 timeout -s KILL 400 rocprofv3 --pmc $c --output-format csv -d $O/pmc_h2_$c -o p -- \
+      python3 bench.py --workload c5 --reading aircomp --steps 1 --warmup 0 $B_FAST --no-check \
+      > $O/pmc_h2_$c.log 2>&1 || return 6
+  done
+  python3 tools/pmc_summary.py $(find $O/pmc_h2_FETCH_SIZE -name "*counter_collection.csv" | head -1) \
+    $(find $O/pmc_h2_WRITE_SIZE -name "*counter_collection.csv" | head -1) $O/pmc_c5air_h2.json \
+    "c5air split" | grep resident_batched
+  # the single-problem kernel's split scope (GMAGG_RES_SPLIT=1) on the grids below the
+  # hierarchical gather's range
+  for r in 1 2; do
+    for sp in 1 0; do
+      GMAGG_RES_SPLIT=$sp timeout -k 10 200 python -u tools/res_shape_bench.py \
+        --shapes 50x20000,50x30000,30x48670,10x48670 --reps 5 | sed "s/}$/, \"split\": $sp}/" >> $O/shapes.jsonl || return 7
+    done
+  done
+  cat $O/shapes.jsonl
+}
+
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 O=gpurun_out/${2:-$1}
 mkdir -p "$O"
