@@ -163,6 +163,29 @@ split() {
   cat $O/shapes.jsonl
 }
 
+c4_pmc() {
+  # Round 5: the whole-C4 Gram partial's clock and MFMA occupancy —
+  # effective clock = GRBM_GUI_ACTIVE / 8 / kernel time, MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES
+  # / (cycles x SIMDs); a kernel trace of the same command for the time
+  A="--workload c4 --steps 2 --warmup 1 $B_FAST --no-check"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o t -- python3 bench.py $A \
+    > $O/trace.json 2> $O/trace.err || { tail -5 $O/trace.err; return 1; }
+  grep -i "gram" $O/trace/t_kernel_stats.csv | cut -c1-200
+  timeout -s KILL 600 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
+    SQ_INSTS_VALU SQ_INSTS_MFMA --output-format csv -d $O/pmc -o p -- python3 bench.py $A > $O/pmc.log 2>&1 || { tail -5 $O/pmc.log; return 2; }
+  python3 - "$O" <<'PY'
+import collections, csv, glob, sys
+o = sys.argv[1]
+f = glob.glob(o + "/pmc/**/*counter_collection.csv", recursive=True)[0]
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
+for r in csv.DictReader(open(f)):
+    if "gram" in r["Kernel_Name"]:
+        acc[r["Kernel_Name"][:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, v in acc.items():
+    print(k, {c: sum(x) / len(x) for c, x in v.items()})
+PY
+}
+
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 O=gpurun_out/${2:-$1}
 mkdir -p "$O"
