@@ -39,6 +39,9 @@
 #ifndef GMK_RES_SLEEP
 #define GMK_RES_SLEEP 1   // spin back-off of the granule polls (A/B knob)
 #endif
+#ifndef GMK_RES_L2SLEEP
+#define GMK_RES_L2SLEEP GMK_RES_SLEEP   // back-off of the hierarchical gather's level-2 polls (A/B)
+#endif
 #ifndef GMK_RES_POLL1
 #define GMK_RES_POLL1 0   // poll one granule per chunk before reading the chunk (A/B knob; 0 was faster)
 #endif
@@ -231,8 +234,8 @@ __device__ __forceinline__ bool gather_pairs(const gu64* g, int64_t gstride, uns
       }
     }
     if (ok) break;
-#if GMK_RES_SLEEP > 0
-    __builtin_amdgcn_s_sleep(GMK_RES_SLEEP);
+#if GMK_RES_L2SLEEP > 0
+    __builtin_amdgcn_s_sleep(GMK_RES_L2SLEEP);
 #endif
     if (((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t0 > kPollTicks) ||
         __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {

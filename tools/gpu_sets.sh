@@ -186,6 +186,56 @@ for k, v in acc.items():
 PY
 }
 
+hier_floor() {
+  # Round 5: the exchange floors of the resident kernel's gathers beyond one XCD (libgmagg_floor.so:
+  # make alt ALT_ONLY=resident ALT_FLAGS=-DGMK_RES_DBG=7) and a longer level-2 poll back-off
+  # (libgmagg_sl4.so: ALT_FLAGS=-DGMK_RES_L2SLEEP=4)
+  for r in 1 2; do
+    for lib in product floor sl4; do
+      L=""; [ $lib != product ] && L="GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$lib.so"
+      for ex in "hier:GMAGG_RES_HIER=2" "split:GMAGG_RES_HIER=0" "flat:GMAGG_RES_HIER=0 GMAGG_RES_SPLIT=0"; do
+        n=${ex%%:*}; e=${ex#*:}
+        env $L $e timeout -k 10 200 python -u tools/res_shape_bench.py --shapes 50x48670,50x20000 --reps 5 \
+          | sed "s/}$/, \"lib\": \"$lib\", \"ex\": \"$n\"}/" >> $O/floor.jsonl || return 3
+      done
+    done
+  done
+  python3 - "$O" <<'PY'
+import collections, json, sys
+acc = collections.defaultdict(list)
+for l in open(sys.argv[1] + "/floor.jsonl"):
+    r = json.loads(l)
+    acc[(r["K"], r["d"], r["lib"], r["ex"])].append(r["us_per_iteration"])
+for k in sorted(acc):
+    print(k, " ".join(f"{v:.2f}" for v in acc[k]))
+PY
+}
+
+poll_ab() {
+  # Round 5: poll pressure of the resident kernel's multi-XCD gathers — variant libraries
+  # (make alt ALT_ONLY=resident ALT_FLAGS=...): libgmagg_sl4all.so -DGMK_RES_SLEEP=4,
+  # libgmagg_sl10all.so -DGMK_RES_SLEEP=10, libgmagg_poll1.so -DGMK_RES_POLL1=1
+  for r in 1 2; do
+    for lib in product sl4all sl10all poll1; do
+      L=""; [ $lib != product ] && L="GMAGG_LIB=byzantine_aircomp_amd/libgmagg_$lib.so"
+      for ex in "auto:GMAGG_RES_HIER=1" "hier:GMAGG_RES_HIER=2" "flat:GMAGG_RES_HIER=0 GMAGG_RES_SPLIT=0"; do
+        n=${ex%%:*}; e=${ex#*:}
+        env $L $e timeout -k 10 200 python -u tools/res_shape_bench.py --shapes 50x7850,50x48670,50x20000 --reps 5 \
+          | sed "s/}$/, \"lib\": \"$lib\", \"ex\": \"$n\"}/" >> $O/poll.jsonl || return 3
+      done
+    done
+  done
+  python3 - "$O" <<'PY'
+import collections, json, sys
+acc = collections.defaultdict(list)
+for l in open(sys.argv[1] + "/poll.jsonl"):
+    r = json.loads(l)
+    acc[(r["K"], r["d"], r["ex"], r["lib"])].append(r["us_per_iteration"])
+for k in sorted(acc):
+    print(k, " ".join(f"{v:.2f}" for v in acc[k]))
+PY
+}
+
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 O=gpurun_out/${2:-$1}
 mkdir -p "$O"
