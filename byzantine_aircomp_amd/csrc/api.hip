@@ -417,12 +417,13 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   // profiles/r5s1_resident_hier_shapes_ab.jsonl, r5s1_resident_hier2_ab.jsonl)
   const int hm = res_hier_mode();
   a.hier = a.stride == 1 && nb > 8 && 2 * K + 2 <= cfg.NW * 64 &&
-           (hm == 2 || (hm == 1 && nb >= 90 && K > 32));
+           (hm == 2 || (hm == 1 && nb >= 90 && K > 32)) && resident_has_exchange(cfg, cpb, 1);
   a.local = (a.stride == 8 || a.hier) && res_xcd_mode() == 2;
   a.lvl2 = a.checkin + nb + 1;
   // below the hierarchical gather's range: the split-scope exchange (one hop, as the flat
   // gather, but each reader polls its own XCD's blocks from L2-kept copies)
-  a.split = a.stride == 1 && !a.hier && nb > 8 && res_xcd_mode() == 2 && res_split_mode() != 0;
+  a.split = a.stride == 1 && !a.hier && nb > 8 && res_xcd_mode() == 2 && res_split_mode() != 0 &&
+            resident_has_exchange(cfg, cpb, 2);
   a.granL = a.lvl2 + (size_t)32 * (2 * K + 2);
   a.bar = bar; a.st = w.st;
   hipEvent_t e0, e1;

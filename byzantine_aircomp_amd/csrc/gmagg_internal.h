@@ -153,6 +153,8 @@ struct ResArgs {
 // grid cannot be co-resident / no kernel for the tile).
 bool resident_plan(const PassCfg& cfg, int64_t nch, int num_cu, int* cpb, int* nb);
 size_t resident_gran_words(int64_t K, const PassCfg& cfg, int nb);
+// whether the resident kernel of this tile has exchange variant xg (1 hierarchical, 2 split)
+bool resident_has_exchange(const PassCfg& cfg, int cpb, int xg);
 hipError_t launch_resident(const PassCfg& cfg, int cpb, int grid, const ResArgs& a, hipStream_t s);
 bool res_coop_launch();   // GMAGG_RES_COOP=1: cooperative launches (resident.hip)
 

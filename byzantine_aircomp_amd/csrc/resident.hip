@@ -258,7 +258,10 @@ __device__ __forceinline__ bool gather_pairs(const gu64* g, int64_t gstride, uns
 template <int NW>
 __host__ __device__ constexpr int64_t res_values(int64_t K) { return 2 * K + 2; }
 
-template <int V, int NW, int LPR, int R, int CPB>
+// EXCH (the exchange, a template parameter so that each variant carries only its own code:
+// C2's one-XCD kernel is the round-4 instruction stream): 0 flat (agent-scope, or L2-kept on
+// one XCD), 1 the XCD-hierarchical gather, 2 the split-scope exchange (api.hip chooses)
+template <int V, int NW, int LPR, int R, int CPB, int EXCH = 0>
 __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   constexpr int QW = 64 / LPR;
   constexpr int NRG = NW * QW;
@@ -294,11 +297,11 @@ __global__ void __launch_bounds__(NW * 64) weiszfeld_resident(ResArgs a) {
   // XCD-hierarchical gather (a.hier, stride 1): group x = the blocks b % 8 == x, which
   // round-robin dispatch places on XCD x; the check-in numbers its slots group by group, so
   // each group's slots are contiguous and its `same` test covers exactly its members
-  const bool hier = a.hier != 0;
+  constexpr bool hier = EXCH == 1;
   // split scope (a.split, stride 1, not hier): one hop as the flat gather, each granule
   // published agent-scope AND L2-kept; a reader polls the L2-kept copies of its own group
   // (XCD) once the check-in confirms the group on one XCD
-  const bool split = a.split != 0 && !hier;
+  constexpr bool split = EXCH == 2;
   const bool xg = hier || split;
   const unsigned XG = hier ? min(8u, nb) : 1u;
   const unsigned grp = xg ? bid % 8u : 0u;
@@ -818,22 +821,28 @@ constexpr bool res_cpb_ok(int V, int NW, int LPR, int R, int CPB) {
 }
 
 template <int V, int NW, int LPR, int R, int CPB>
-static const void* res_fn() {
-  if constexpr (res_cpb_ok(V, NW, LPR, R, CPB))
-    return reinterpret_cast<const void*>(&weiszfeld_resident<V, NW, LPR, R, CPB>);
-  else
-    return nullptr;
+static const void* res_fn(int xg) {
+  // the hierarchical / split-scope variants exist for the 8-wave tile (32 < K <= 64, where
+  // they measured faster); every other tile gathers flat beyond one XCD
+  if constexpr (res_cpb_ok(V, NW, LPR, R, CPB)) {
+    if (xg == 0) return reinterpret_cast<const void*>(&weiszfeld_resident<V, NW, LPR, R, CPB>);
+    if constexpr (NW == 8 && LPR == 64 && R == 8) {
+      if (xg == 1) return reinterpret_cast<const void*>(&weiszfeld_resident<V, NW, LPR, R, CPB, 1>);
+      if (xg == 2) return reinterpret_cast<const void*>(&weiszfeld_resident<V, NW, LPR, R, CPB, 2>);
+    }
+  }
+  return nullptr;
 }
 
-static const void* resident_kernel(const PassCfg& cfg, int cpb) {
+static const void* resident_kernel(const PassCfg& cfg, int cpb, int xg = 0) {
 #define GMK_RES(V_, W_, L_, R_)                                              \
   if (cfg.V == V_ && cfg.NW == W_ && cfg.LPR == L_ && cfg.R == R_) {         \
     switch (cpb) {                                                           \
-      case 1: return res_fn<V_, W_, L_, R_, 1>();                            \
-      case 2: return res_fn<V_, W_, L_, R_, 2>();                            \
-      case 3: return res_fn<V_, W_, L_, R_, 3>();                            \
-      case 4: return res_fn<V_, W_, L_, R_, 4>();                            \
-      case 8: return res_fn<V_, W_, L_, R_, 8>();                            \
+      case 1: return res_fn<V_, W_, L_, R_, 1>(xg);                          \
+      case 2: return res_fn<V_, W_, L_, R_, 2>(xg);                          \
+      case 3: return res_fn<V_, W_, L_, R_, 3>(xg);                          \
+      case 4: return res_fn<V_, W_, L_, R_, 4>(xg);                          \
+      case 8: return res_fn<V_, W_, L_, R_, 8>(xg);                          \
       default: return nullptr;                                               \
     }                                                                        \
   }
@@ -893,8 +902,12 @@ bool res_coop_launch() {
   return coop;
 }
 
+bool resident_has_exchange(const PassCfg& cfg, int cpb, int xg) {
+  return resident_kernel(cfg, cpb, xg) != nullptr;
+}
+
 hipError_t launch_resident(const PassCfg& cfg, int cpb, int grid, const ResArgs& a, hipStream_t s) {
-  const void* fn = resident_kernel(cfg, cpb);
+  const void* fn = resident_kernel(cfg, cpb, a.hier ? 1 : a.split ? 2 : 0);
   if (!fn) return hipErrorInvalidValue;
   void* args[] = {const_cast<ResArgs*>(&a)};
   // A plain launch by default: co-residency is established by resident_plan's occupancy

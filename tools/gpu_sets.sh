@@ -236,6 +236,15 @@ for k in sorted(acc):
 PY
 }
 
+c2_ab() {
+  # C2's resident kernel, this build against libgmagg_r4res.so (the round-4 resident.hip linked
+  # with the same other objects): interleaved bench A/B, three rounds
+  timeout -k 10 900 python -u tools/ab.py --rounds 3 --bench=--workload,c2,--no-cpu,--alt-steps,0,--soak,0 \
+    --variant now= --variant r4=GMAGG_LIB=byzantine_aircomp_amd/libgmagg_r4res.so --out $O/ab_c2.jsonl \
+    > $O/ab_c2.log 2>&1 || { tail -20 $O/ab_c2.log; return 1; }
+  tail -2 $O/ab_c2.log
+}
+
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 O=gpurun_out/${2:-$1}
 mkdir -p "$O"
