@@ -266,9 +266,9 @@ __device__ __forceinline__ int wave_scan_i32(int v) {
 // it saved.  buf(c, q): LDS slots of chain (c, q), STR words apart, >= 64*R2 of them.
 template <int R, int NC, int NR, int R2, int STR, typename Buf>
 __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const int64_t (&r)[NR],
-                                             uint32_t (&ans)[NC][NR], Buf buf) {
+                                             uint32_t (&ans)[NC][NR], int (&clo)[NC][NR],
+                                             int (&chi)[NC][NR], Buf buf) {
   constexpr bool COMPACT = R2 > 0 && R > R2;
-  int clo[NC][NR], chi[NC][NR];
   int rr[NR];
 #pragma unroll
   for (int q = 0; q < NR; ++q) rr[q] = (int)r[q];   // counts fit 32 bits (K <= 2048)
@@ -779,11 +779,10 @@ __device__ __forceinline__ bool median_vhist(const uint32_t (&key)[2][R], int rr
 // l + 64 i): res[h] = the median (mode 0) or the trimmed mean (mode 1) of column h.
 // buf(h, q): LDS slots for chain (h, q)'s compaction, STR words apart.
 // NCOL = 1: one column per wave (col_select1).
-template <int R, int R2, int STR, int NCOL = 2, typename Buf>
+template <int MODE, int R, int R2, int STR, int NCOL = 2, typename Buf>
 __device__ __forceinline__ void select_pair(const uint32_t (&key)[NCOL][R], const bool (&nan)[NCOL],
-                                            int64_t K, int mode, int64_t b, Buf buf,
-                                            float (&res)[NCOL]) {
-  if (mode == 0) {
+                                            int64_t K, int64_t b, Buf buf, float (&res)[NCOL]) {
+  if constexpr (MODE == 0) {
     const int64_t rk[1] = {(K - 1) / 2};
     uint32_t ans[NCOL][1];
     bool done = false;
@@ -797,14 +796,18 @@ __device__ __forceinline__ void select_pair(const uint32_t (&key)[NCOL][R], cons
         }
       }
     }
-    if (!done) select_ranks<R, NCOL, 1, R2, STR>(key, rk, ans, buf);
+    if (!done) {
+      int clo[NCOL][1], chi[NCOL][1];
+      select_ranks<R, NCOL, 1, R2, STR>(key, rk, ans, clo, chi, buf);
+    }
 #pragma unroll
     for (int h = 0; h < NCOL; ++h)
       res[h] = __ballot(nan[h]) ? __uint_as_float(0x7FC00000u) : key_value(ans[h][0]);
   } else {
     const int64_t rk[2] = {b, K - b - 1};
     uint32_t ans[NCOL][2];
-    select_ranks<R, NCOL, 2, R2, STR>(key, rk, ans, buf);
+    int clo[NCOL][2], chi[NCOL][2];
+    select_ranks<R, NCOL, 2, R2, STR>(key, rk, ans, clo, chi, buf);
     const int64_t n = K - 2 * b;
 #pragma unroll
     for (int h = 0; h < NCOL; ++h) {
@@ -814,14 +817,18 @@ __device__ __forceinline__ void select_pair(const uint32_t (&key)[NCOL][R], cons
       if (lo == hi) {
         sum = (double)n * (double)vlo;
       } else {
-        double sv = 0.0;
-        int64_t le_lo = 0, lt_hi = 0;
+        // the selection's final intervals hold the boundary counts (round 5): rank b's
+        // interval is [lo, lo + 1) or a one-key interval, so #(keys <= lo) = chi, and
+        // #(keys < hi) = rank K-b-1's clo (padding keys count on both sides alike)
+        double sv0 = 0.0, sv1 = 0.0;
+        const int64_t le_lo = chi[h][0], lt_hi = clo[h][1];
 #pragma unroll
-        for (int i = 0; i < R; ++i) {
-          if (key[h][i] > lo && key[h][i] < hi) sv += (double)key_value(key[h][i]);
-          le_lo += __popcll(__ballot(key[h][i] <= lo));
-          lt_hi += __popcll(__ballot(key[h][i] < hi));
+        for (int i = 0; i < R; i += 2) {
+          if (key[h][i] > lo && key[h][i] < hi) sv0 += (double)key_value(key[h][i]);
+          if (i + 1 < R && key[h][i + 1] > lo && key[h][i + 1] < hi)
+            sv1 += (double)key_value(key[h][i + 1]);
         }
+        double sv = sv0 + sv1;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) sv += __shfl_xor(sv, o);
         sum = sv + (double)(le_lo - b) * (double)vlo + (double)((K - b) - lt_hi) * (double)vhi;
@@ -832,9 +839,9 @@ __device__ __forceinline__ void select_pair(const uint32_t (&key)[NCOL][R], cons
 }
 
 // The selection of one staged K x C tile (columns j0 .. j0 + C - 1).
-template <int R, int C, int NWV>
+template <int MODE, int R, int C, int NWV>
 __device__ __forceinline__ void select_tile(float (&tile)[64 * R][C + 1], int64_t K, int64_t d,
-                                            int64_t j0, int mode, int64_t b,
+                                            int64_t j0, int64_t b,
                                             float* __restrict__ out) {
   // wave w selects columns in pairs (w + 2m NWV, w + 2m NWV + NWV): C % (2 NWV) == 0
   static_assert(C % (2 * NWV) == 0, "column pairs");
@@ -860,7 +867,7 @@ __device__ __forceinline__ void select_tile(float (&tile)[64 * R][C + 1], int64_
     auto buf = [&](int h, int q) {
       return reinterpret_cast<uint32_t*>(&tile[q * 64 * (R2 > 0 ? R2 : 1)][c0 + NWV * h]);
     };
-    select_pair<R, R2, C + 1>(key, nan, K, mode, b, buf, res);
+    select_pair<MODE, R, R2, C + 1>(key, nan, K, b, buf, res);
     if (lane == 0) {
       out[j0 + c0] = res[0];
       if (j0 + c0 + NWV < d) out[j0 + c0 + NWV] = res[1];
@@ -876,10 +883,10 @@ __device__ __forceinline__ void select_tile(float (&tile)[64 * R][C + 1], int64_
 // loading tile t + grid into registers while its waves select tile t's columns, so the
 // loads of a CU are in flight during its selection instead of only between tiles (the
 // plain form: one tile per block, loads then selection).
-template <int R, int C, int NWV, bool PERSIST>
+template <int MODE, int R, int C, int NWV, bool PERSIST>
 __global__ void __launch_bounds__(NWV * 64) col_select(const float* __restrict__ X, int64_t K,
-                                                  int64_t d, int64_t ldx, int ws, int mode,
-                                                  int64_t b, int vec4, float* __restrict__ out) {
+                                                  int64_t d, int64_t ldx, int ws, int64_t b,
+                                                  int vec4, float* __restrict__ out) {
   __shared__ float tile[64 * R][C + 1];
   const int64_t ntiles = (d + C - 1) / C;
   typedef float f4 __attribute__((ext_vector_type(4)));
@@ -937,7 +944,7 @@ __global__ void __launch_bounds__(NWV * 64) col_select(const float* __restrict__
     if constexpr (GMK_SELECT_DBG == 1) {
       if (threadIdx.x < C && j0 + threadIdx.x < d) out[j0 + threadIdx.x] = tile[threadIdx.x][threadIdx.x];
     } else {
-      select_tile<R, C, NWV>(tile, K, d, j0, mode, b, out);
+      select_tile<MODE, R, C, NWV>(tile, K, d, j0, b, out);
     }
   }
 }
@@ -946,10 +953,9 @@ __global__ void __launch_bounds__(NWV * 64) col_select(const float* __restrict__
 // column w alone, so that a wave holds 16 keys instead of 32 and the kernel fits 64 VGPRs:
 // 8 waves per SIMD instead of 4, to hide the per-step compare -> count -> decide latency
 // that bounds the pair kernel.  Loads: 4 float4 per thread in flight.
-template <int R, int C>
+template <int MODE, int R, int C>
 __global__ void __launch_bounds__(C * 64, 2) col_select1(const float* __restrict__ X, int64_t K,
-                                                      int64_t d, int64_t ldx, int ws, int mode,
-                                                      int64_t b, int vec4,
+                                                      int64_t d, int64_t ldx, int ws, int64_t b, int vec4,
                                                       float* __restrict__ out) {
   __shared__ float tile[64 * R][C + 1];
   typedef float f4 __attribute__((ext_vector_type(4)));
@@ -1007,7 +1013,7 @@ __global__ void __launch_bounds__(C * 64, 2) col_select1(const float* __restrict
     return reinterpret_cast<uint32_t*>(&tile[q * 64 * (R2 > 0 ? R2 : 1)][w]);
   };
   float res[1];
-  select_pair<R, R2, C + 1, 1>(key, nan, K, mode, b, bufc, res);
+  select_pair<MODE, R, R2, C + 1, 1>(key, nan, K, b, bufc, res);
   if (lane == 0) out[j0 + w] = res[0];
 }
 
@@ -1225,18 +1231,36 @@ hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, 
       occ = 1;
     return (unsigned)(cus * occ);
   };
-#define GMK_SEL(R, C, NWV)                                                                      \
+  // the two modes are separate kernels (round 5): as one kernel with a runtime mode, the
+  // trimmed mean's tail set the median's registers and schedule (K=256 median 1.20 -> 1.55 ms
+  // when the trimmed mean's tail changed, profiles/r5s2_select_tm_ab.jsonl)
+#define GMK_SEL_M(M, R, C, NWV)                                                                 \
   do {                                                                                          \
     const int64_t nt_ = (d + C - 1) / C;                                                        \
     if (persist) {                                                                              \
-      const unsigned g_ = resident(reinterpret_cast<const void*>(&col_select<R, C, NWV, true>),   \
+      const unsigned g_ = resident(reinterpret_cast<const void*>(&col_select<M, R, C, NWV, true>), \
                                    NWV * 64);                                                   \
-      hipLaunchKernelGGL((col_select<R, C, NWV, true>), dim3((unsigned)std::min<int64_t>(nt_, g_)), \
-                         dim3(NWV * 64), 0, s, X, K, d, ldx, ws, mode, b, vec4, out);            \
+      hipLaunchKernelGGL((col_select<M, R, C, NWV, true>),                                      \
+                         dim3((unsigned)std::min<int64_t>(nt_, g_)), dim3(NWV * 64), 0, s, X, K, \
+                         d, ldx, ws, b, vec4, out);                                             \
     } else {                                                                                    \
-      hipLaunchKernelGGL((col_select<R, C, NWV, false>), dim3((unsigned)nt_), dim3(NWV * 64), 0, \
-                         s, X, K, d, ldx, ws, mode, b, vec4, out);                              \
+      hipLaunchKernelGGL((col_select<M, R, C, NWV, false>), dim3((unsigned)nt_), dim3(NWV * 64), \
+                         0, s, X, K, d, ldx, ws, b, vec4, out);                                 \
     }                                                                                           \
+  } while (0)
+#define GMK_SEL(R, C, NWV)                                                                      \
+  do {                                                                                          \
+    if (mode == 0) GMK_SEL_M(0, R, C, NWV);                                                     \
+    else GMK_SEL_M(1, R, C, NWV);                                                               \
+  } while (0)
+#define GMK_SEL1(R, C)                                                                          \
+  do {                                                                                          \
+    if (mode == 0)                                                                              \
+      hipLaunchKernelGGL((col_select1<0, R, C>), dim3((unsigned)((d + C - 1) / C)), dim3(C * 64), \
+                         0, s, X, K, d, ldx, ws, b, vec4, out);                                 \
+    else                                                                                        \
+      hipLaunchKernelGGL((col_select1<1, R, C>), dim3((unsigned)((d + C - 1) / C)), dim3(C * 64), \
+                         0, s, X, K, d, ldx, ws, b, vec4, out);                                 \
   } while (0)
   // (round 4: gathering each wave's column pair straight from HBM, no LDS tile, so that
   // VGPRs rather than two 69.6-KB tiles limit the CU: K=1000 x 2M median 21.0 vs 3.83 ms —
@@ -1259,19 +1283,19 @@ hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, 
   // 1.26 ms at K=256 x 2M), the trimmed mean loses (2.24 -> 2.36); GMAGG_SELECT_1COL=2
   // puts both there (profiles/r4s2_select_1col_k256_ab.jsonl)
   else if (K <= 256 && (one_col_env < 0 ? mode == 0 : one_col_env == 2)) {
-    hipLaunchKernelGGL((col_select1<4, 16>), dim3((unsigned)((d + 15) / 16)), dim3(1024), 0, s, X,
-                       K, d, ldx, ws, mode, b, vec4, out);
+    GMK_SEL1(4, 16);
   }
   else if (K <= 256) GMK_SEL(4, 32, 4);
   else if (K <= 512) GMK_SEL(8, 16, 4);
   else if (K <= 1024 && one_col) {
-    hipLaunchKernelGGL((col_select1<16, 16>), dim3((unsigned)((d + 15) / 16)), dim3(1024), 0, s, X,
-                       K, d, ldx, ws, mode, b, vec4, out);
+    GMK_SEL1(16, 16);
   }
   else if (K <= 1024) GMK_SEL(16, 16, 8);
   else if (K <= 2048) GMK_SEL(32, 8, 4);
   else return hipErrorInvalidValue;
 #undef GMK_SEL
+#undef GMK_SEL_M
+#undef GMK_SEL1
   return hipGetLastError();
 }
 

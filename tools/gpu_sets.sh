@@ -245,6 +245,22 @@ c2_ab() {
   tail -2 $O/ab_c2.log
 }
 
+f3_ab() {
+  # f3 selection: this build against libgmagg_old.so (the previous build, copied aside):
+  # the f3 GPU tests, then select_bench interleaved, three rounds
+  timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+    tests/test_gpu_other_aggregators.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  for r in 1 2 3; do
+    for lib in new old; do
+      L=""; [ $lib = old ] && L="GMAGG_LIB=byzantine_aircomp_amd/libgmagg_old.so"
+      env $L timeout -k 10 120 python -u tools/select_bench.py --K 1000 256 --reps 5 \
+        | sed "s/}$/, \"lib\": \"$lib\"}/" >> $O/sel.jsonl || return 2
+    done
+  done
+  cat $O/sel.jsonl
+}
+
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 O=gpurun_out/${2:-$1}
 mkdir -p "$O"
