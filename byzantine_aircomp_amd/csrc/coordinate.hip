@@ -247,6 +247,9 @@ __device__ __forceinline__ int wave_scan_i32(int v) {
 #ifndef GMK_SELECT_HIST
 #define GMK_SELECT_HIST 2
 #endif
+#ifndef GMK_SELECT_NBALLOT
+#define GMK_SELECT_NBALLOT 0
+#endif
 #ifndef GMK_SELECT_HIST_NR
 #define GMK_SELECT_HIST_NR 2
 #endif
@@ -284,26 +287,32 @@ __device__ __forceinline__ void select_ranks(const uint32_t (&key)[NC][R], const
   // scalar popcount, a scalar add) and the loop is issue-bound (one instruction per
   // wave per cycle slot), so at R >= 8 each lane counts its own keys instead (v_cmp +
   // v_addc: two) and two chains share one DPP wave sum (16-bit halves: <= 2048 each).
+  // GMK_SELECT_NBALLOT (A/B knob): the first NB keys of each lane counted by ballot
+  // (1 VALU + 2 SALU per key) and the rest per lane (2 VALU), to balance the two issue ports
   auto full = [&](const uint32_t (&t)[NC][NR], int (&cnt)[NC][NR]) {
     if constexpr (R >= 8) {
-      int lc[NC * NR];
+      constexpr int NB = GMK_SELECT_NBALLOT < R ? GMK_SELECT_NBALLOT : R - 1;
+      int lc[NC * NR], sc[NC * NR];
 #pragma unroll
       for (int c = 0; c < NC; ++c)
 #pragma unroll
         for (int q = 0; q < NR; ++q) {
-          int v = 0;
+          int v = 0, sb = 0;
 #pragma unroll
-          for (int i = 0; i < R; ++i) v += (int)(key[c][i] < t[c][q]);
+          for (int i = 0; i < NB; ++i) sb += __popcll(__ballot(key[c][i] < t[c][q]));
+#pragma unroll
+          for (int i = NB; i < R; ++i) v += (int)(key[c][i] < t[c][q]);
           lc[c * NR + q] = v;
+          sc[c * NR + q] = sb;
         }
 #pragma unroll
       for (int p = 0; p < NC * NR; p += 2) {
         if (p + 1 < NC * NR) {
           const int s2 = wave_sum_i32(lc[p] + (lc[p + 1] << 16));
-          cnt[p / NR][p % NR] = s2 & 0xFFFF;
-          cnt[(p + 1) / NR][(p + 1) % NR] = s2 >> 16;
+          cnt[p / NR][p % NR] = (s2 & 0xFFFF) + sc[p];
+          cnt[(p + 1) / NR][(p + 1) % NR] = (s2 >> 16) + sc[p + 1];
         } else {
-          cnt[p / NR][p % NR] = wave_sum_i32(lc[p]);   // (an odd chain count: NC = NR = 1)
+          cnt[p / NR][p % NR] = wave_sum_i32(lc[p]) + sc[p];   // (an odd chain count: NC = NR = 1)
         }
       }
     } else {

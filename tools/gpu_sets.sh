@@ -261,6 +261,32 @@ f3_ab() {
   cat $O/sel.jsonl
 }
 
+tm_variants() {
+  # the trimmed mean's selection after the round-5 tail change: the one-column kernel against
+  # the column-pair one (GMAGG_SELECT_1COL=0), and the histogram schedule (libgmagg_h1.so:
+  # make alt ALT_ONLY=coordinate ALT_FLAGS=-DGMK_SELECT_HIST=1, libgmagg_h0.so: =0), and the
+  # counting steps' ballot share (libgmagg_nbN.so: ALT_FLAGS=-DGMK_SELECT_NBALLOT=N)
+  for r in 1 2; do
+    for v in "def:" "pair:GMAGG_SELECT_1COL=0" "h1:GMAGG_LIB=byzantine_aircomp_amd/libgmagg_h1.so" \
+             "h0:GMAGG_LIB=byzantine_aircomp_amd/libgmagg_h0.so" \
+             "h1pair:GMAGG_LIB=byzantine_aircomp_amd/libgmagg_h1.so GMAGG_SELECT_1COL=0" \
+             "nb4:GMAGG_LIB=byzantine_aircomp_amd/libgmagg_nb4.so" "nb8:GMAGG_LIB=byzantine_aircomp_amd/libgmagg_nb8.so"; do
+      n=${v%%:*}; e=${v#*:}
+      env $e timeout -k 10 120 python -u tools/select_bench.py --K 1000 256 --reps 5 \
+        | sed "s/}$/, \"v\": \"$n\"}/" >> $O/sel.jsonl || return 2
+    done
+  done
+  python3 - "$O" <<'PY'
+import collections, json, sys
+acc = collections.defaultdict(list)
+for l in open(sys.argv[1] + "/sel.jsonl"):
+    r = json.loads(l)
+    acc[(r["agg"], r["K"], r["v"])].append(r["ms"])
+for k in sorted(acc):
+    print(k, " ".join(f"{v:.3f}" for v in acc[k]))
+PY
+}
+
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 O=gpurun_out/${2:-$1}
 mkdir -p "$O"
