@@ -85,6 +85,7 @@ SIGNATURES = [
     ("gm_median_panels_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _P, _P]),
     ("gm_trimmed_mean_panels_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _I64, _P, _P]),
     ("gm_krum_panels_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _I64, _P, C.POINTER(_I64), _P]),
+    ("gm_krum_last_info", C.c_int, [_P, C.POINTER(_I64)]),
     ("gm_oma_philox_f32", C.c_int, [_P, _P, _I64, _I64, _I64, C.c_double, C.c_uint64, _P]),
     ("gm_honest_variance_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _P, _P]),
     ("gm_honest_variance_panels_f32", C.c_int, [_P, _P, _I64, _I64, _I64, _I64, _P, _P]),

@@ -369,7 +369,12 @@ def Krum(wList, options):  # noqa: N802 - reference name (M:197)
         _lib.check(getattr(ctx.lib, fn)(ctx.handle, X.data_ptr(), K, d, ldx,
                                         int(options["honestSize"]), out.data_ptr(), C.byref(idx),
                                         _stream_ptr(X.device)), fn)
+    info = (C.c_int64 * 3)()
+    _lib.check(ctx.lib.gm_krum_last_info(ctx.handle, info), "gm_krum_last_info")
     Krum.last_index = idx.value
+    Krum.last_info = {"algo": ("exact", "gram")[info[0]], "candidates": info[1],
+                      "reason": ("ok", "not_chosen", "not_eligible", "gram_nonfinite",
+                                 "candidates")[info[2]]}
     return out if wList.device == out.device else out.to(wList.device)
 
 

@@ -77,6 +77,8 @@ struct gm_ctx {
   // grid_checkin: a shared GPU, CUs held by another stream) makes the next calls stream
   // straight away instead of paying the check-in's 100 ms again; retried after this many.
   int res_skip = 0;
+  // the last Krum call (gm_krum_last_info): {algorithm, candidates, reason}
+  int64_t krum_info[3] = {GM_KRUM_EXACT, 0, GM_KRUM_REASON_NOT_CHOSEN};
 };
 
 namespace {
@@ -1599,11 +1601,127 @@ int gm_krum_panels_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t 
   return krum_impl(c, X, K, d, panel_stride, ws, honest, out, index, stream);
 }
 
+// Krum through the Gram MFMA kernel (coordinate.hip krum_gram_bounds: the bounds, the
+// candidates, the exact recomputation).  epsg bounds |G~_ij - G_ij| / (n_i n_j) for the
+// scaled-f16 split (gram.hip): the split's dropped terms (<= 3 * 2^-22), the fp32 chain of
+// one flush period (kH16Flush stages x 64 columns = 8192 columns, 3 products: <= 768
+// accumulator roundings + the 32-term MFMA sums + the fp32 partial, <= 800 * 2^-24), the
+// centring rounding (2^-24 each side) and the f16 subnormal floor (2^-27 of the row's
+// largest element per element: <= 2^-27 sqrt(d) by Cauchy-Schwarz), rounded up to 6e-5.
+static double krum_gram_eps(int64_t d) {
+  return 6e-5 + std::ldexp(1.0, -27) * std::sqrt((double)d);
+}
+
+// GMAGG_KRUM: 0 exact pair distances only, 1 the Gram path wherever it is eligible, 2
+// (default) AUTO: the Gram path at K >= 64 and K^2 d >= 2^29 (it measured faster on every
+// shape from 64 x 131,072 up, profiles/r5s2_krum_ab.jsonl).  Read per call (the tests
+// switch it).
+static int krum_mode() {
+  const char* e = getenv("GMAGG_KRUM");
+  return e ? atoi(e) : 2;
+}
+
+// Returns GM_OK with *done = false when the exact path must run (not eligible, a
+// non-finite Gram, too many candidates), c->krum_info saying why.
+static int krum_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, int ws,
+                     int64_t honest, float* out, int64_t* index, hipStream_t s, bool* done) {
+  *done = false;
+  const int KT = gram_kt(K), KP = 32 * KT;
+  const int64_t kk = honest - 1;
+  const GramGrid gg = gram_grid(d, GramKind::H16, c->num_cu);
+  const int64_t S = krum_slices(K, d);
+  const int64_t RC = krum_refine_max();
+  const int64_t maxc = 4 * RC;
+  // slab: the Gram partials, then (after gram_reduce has consumed them) the refinement's
+  // [S][RC][K] fp64 partials + Dc [RC][K]; behind both the candidate list (int64)
+  size_t body = std::max(gram_slab_floats(KT, gg), (size_t)2 * (size_t)(S * RC * K + RC * K));
+  body = (body + 1) / 2 * 2;
+  Workspace w;
+  int rc = ensure_ws(c, K, d, 1, &w, body + 2 * (size_t)(maxc + 2), KP);
+  if (rc) return rc;
+  rc = ensure_host(c, sizeof(KState) + 2 * sizeof(int64_t));
+  if (rc) return rc;
+  double* part = reinterpret_cast<double*>(w.gslab);
+  double* Dc = part + (size_t)S * RC * K;
+  int64_t* cand = reinterpret_cast<int64_t*>(w.gslab + body);
+  int64_t* didx = reinterpret_cast<int64_t*>(w.r);
+  KState* hst = reinterpret_cast<KState*>(c->host);
+  int64_t* hcand = reinterpret_cast<int64_t*>(c->host + sizeof(KState));
+  const int64_t W = ws ? (int64_t)1 << ws : 0;
+  // The bounds scale with the rows' distances from the centre p: row 0 first (honest in
+  // the reference's layout, M:292); when it leaves too many candidates (a Byzantine row 0,
+  // far from the honest cluster) once more from the row of the smallest upper bound.
+  int64_t n = 0, centre = 0;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    float* p = w.g[1];
+    HIPCHK(launch_copy_row_k(X, d, ldx, ws, centre, p, s));
+    HIPCHK(hipMemsetAsync(w.st, 0, sizeof(KState), s));
+    HIPCHK(launch_gram(X, K, d, ws ? W : ldx, p, GramKind::H16, gg, w.gslab, w.G, w.st, s,
+                       ws ? ldx : 0, ws));
+    HIPCHK(launch_gram_check(w.G, KP, w.st, s));
+    HIPCHK(launch_krum_gram_select(w.G, KP, K, kk, krum_gram_eps(d), w.alpha, w.u, maxc, cand, s));
+    HIPCHK(hipMemcpyAsync(hst, w.st, sizeof(KState), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hcand, cand, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hcand + 1, cand + maxc + 1, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (hst->gram_bad) {
+      c->krum_info[2] = GM_KRUM_REASON_GRAM_NONFINITE;
+      return GM_OK;
+    }
+    n = hcand[0];
+    if (n != -2 || hcand[1] == centre) break;
+    centre = hcand[1];
+  }
+  if (n < 1) {
+    c->krum_info[2] = GM_KRUM_REASON_CANDIDATES;
+    return GM_OK;
+  }
+  for (int64_t q = 0; q < n; q += RC) {
+    const int m = (int)std::min<int64_t>(RC, n - q);
+    HIPCHK(launch_krum_refine(X, K, d, ldx, ws, cand + 1 + q, m, kk, part, Dc, w.sums + q, s));
+  }
+  HIPCHK(launch_krum_pick(w.sums, cand + 1, n, X, d, ldx, ws, didx, out, s));
+  if (index) {
+    HIPCHK(hipMemcpyAsync(index, didx, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  c->krum_info[0] = GM_KRUM_GRAM;
+  c->krum_info[1] = n;
+  c->krum_info[2] = GM_KRUM_REASON_OK;
+  *done = true;
+  return GM_OK;
+}
+
+int gm_krum_last_info(gm_ctx* c, int64_t* info) {
+  if (!c || !info) return fail(GM_ERR_INVALID, "gm_krum_last_info: bad args");
+  for (int i = 0; i < 3; ++i) info[i] = c->krum_info[i];
+  return GM_OK;
+}
+
 static int krum_impl(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx, int ws,
                      int64_t honest, float* out, int64_t* index, void* stream) {
   HIPCHK(hipSetDevice(c->device));
-  WsOrder order(c, reinterpret_cast<hipStream_t>(stream));
+  const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  WsOrder order(c, s);
   HIPCHK(order.err);
+  c->krum_info[0] = GM_KRUM_EXACT;
+  c->krum_info[1] = 0;
+  c->krum_info[2] = GM_KRUM_REASON_NOT_CHOSEN;
+  // the Gram kernel's inputs: K <= 256; rows 16-byte aligned with d, ldx multiples of 4
+  // (float4 stages); panels of width 64 / 128 / 256 (a power of two, multiple of 64)
+  const bool eligible =
+      gram_kt(K) > 0 && d > 0 && honest - 1 <= K &&
+      (ws ? (ws >= 6 && ws <= 8 && K * ((int64_t)1 << ws) * 4 <= 0x7fffffff)
+          : (d % 4 == 0 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
+             ldx < ((int64_t)1 << 26)));
+  const int mode = krum_mode();
+  const bool want = mode == 1 || (mode == 2 && K >= 64 && (double)K * K * d >= 536870912.0);
+  if (want && !eligible) c->krum_info[2] = GM_KRUM_REASON_NOT_ELIGIBLE;
+  if (want && eligible) {
+    bool done = false;
+    const int rc = krum_gram(c, X, K, d, ldx, ws, honest, out, index, s, &done);
+    if (rc || done) return rc;
+  }
   Workspace w;
   // G area holds the K x K distances; the float slab holds the per-slice fp64 partials
   const size_t part_doubles = (size_t)krum_slices(K, d) * (size_t)(K * K);

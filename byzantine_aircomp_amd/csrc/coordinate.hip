@@ -1157,6 +1157,22 @@ __global__ void __launch_bounds__(256) pair_reduce(const double* __restrict__ pa
   if (w == 0 && on) D[e] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
+// The sum of the kk smallest entries of a row staged in LDS (stable rank), summed per
+// thread in j order and over the block by block_sum: every Krum score — the exact path's
+// and the Gram path's refined candidates' — goes through this one function, so equal rows
+// give equal bits.
+__device__ __forceinline__ double krum_row_score(const double* srow, int64_t K, int64_t kk,
+                                                 double* scratch) {
+  double sc = 0.0;
+  for (int64_t j = threadIdx.x; j < K; j += blockDim.x) {
+    const double x = srow[j];
+    int64_t rank = 0;
+    for (int64_t t = 0; t < K; ++t) rank += (srow[t] < x) || (srow[t] == x && t < j);
+    if (rank < kk) sc += x;
+  }
+  return block_sum(sc, scratch);
+}
+
 // Krum, step 2 (one block per row): score_i = sum of the kk smallest D[i][*] (self
 // included, M:200-201), by stable rank over the row staged in LDS.
 __global__ void __launch_bounds__(256) krum_score(const double* __restrict__ D, int64_t K,
@@ -1166,14 +1182,7 @@ __global__ void __launch_bounds__(256) krum_score(const double* __restrict__ D, 
   const int64_t i = blockIdx.x;
   for (int64_t j = threadIdx.x; j < K; j += blockDim.x) srow[j] = D[i <= j ? i * K + j : j * K + i];
   __syncthreads();
-  double sc = 0.0;
-  for (int64_t j = threadIdx.x; j < K; j += blockDim.x) {
-    const double x = srow[j];
-    int64_t rank = 0;
-    for (int64_t t = 0; t < K; ++t) rank += (srow[t] < x) || (srow[t] == x && t < j);
-    if (rank < kk) sc += x;
-  }
-  sc = block_sum(sc, scratch);
+  const double sc = krum_row_score(srow, K, kk, scratch);
   if (threadIdx.x == 0) score[i] = sc;
 }
 
@@ -1199,6 +1208,251 @@ __global__ void __launch_bounds__(256) copy_row(const float* __restrict__ X, int
                                                 const int64_t* __restrict__ index,
                                                 float* __restrict__ out) {
   const int64_t k = *index;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < d;
+       c += (int64_t)gridDim.x * blockDim.x)
+    out[c] = *elem(X, ldx, ws, k, c);
+}
+
+// ---------------------------------------------------------------------------
+// Krum through the Gram MFMA kernel (round 5; SURVEY §8 f3: D = diag(G) 1^T + 1 diag(G)^T
+// - 2G).  G~ = (X - p)(X - p)^T from gram.hip's scaled-f16 split (p = row 0), then
+//   D~_ij = G~_ii + G~_jj - 2 G~_ij,  |D_ij - D~_ij| <= e_ij = epsg (n_i + n_j)^2 + 1e-5 |D~_ij|
+// (n_i = ||x_i - p||; epsg bounds |G~ - G| / (n_i n_j): the split's 2^-22 terms, the fp32
+// accumulation chains between flushes, the f16 subnormal floor — api.hip krum_gram_eps; the
+// 1e-5 |D~| covers the exact path's own fp32 rounding).  A row's score is the sum of its kk
+// smallest distances (self = 0), monotone in each distance, so
+//   LB_i = score(max(0, D~ - e)) <= score_i <= UB_i = score(D~ + e).
+// Every row with LB_i <= min_j UB_j is a candidate — the exact argmin always is — and the
+// candidates' distance rows are recomputed with the exact path's arithmetic (same slices,
+// 32-column fp32 stages, fp64 across stages, pair_reduce's order, krum_row_score): their
+// scores carry the exact path's bits, so the index equals the exact path's.
+
+// One block per row i: LB_i, UB_i.  A bound that cannot hold (D~ + e < 0, a non-finite G)
+// gives NaN, which sends the call to the exact path.
+__global__ void __launch_bounds__(256) krum_gram_bounds(const double* __restrict__ G, int KP,
+                                                        int64_t K, int64_t kk, double epsg,
+                                                        double* __restrict__ lb,
+                                                        double* __restrict__ ub) {
+  extern __shared__ double sb[];
+  double* sl = sb;
+  double* su = sb + K;
+  __shared__ double scratch[8];
+  const int64_t i = blockIdx.x;
+  const double gii = G[i * KP + i];
+  const double ni = sqrt(fmax(gii, 0.0) * (1.0 + 2.0 * epsg));
+  for (int64_t j = threadIdx.x; j < K; j += blockDim.x) {
+    const double gjj = G[j * KP + j];
+    const double nj = sqrt(fmax(gjj, 0.0) * (1.0 + 2.0 * epsg));
+    const double dt = (gii + gjj) - 2.0 * G[i * KP + j];
+    const double e = epsg * (ni + nj) * (ni + nj) + 1e-5 * fabs(dt);
+    const double hi = dt + e;
+    sl[j] = j == i ? 0.0 : fmax(dt - e, 0.0);
+    su[j] = j == i ? 0.0 : (hi >= 0.0 ? hi : __builtin_nan(""));
+  }
+  __syncthreads();
+  const double l = krum_row_score(sl, K, kk, scratch);
+  const double u = krum_row_score(su, K, kk, scratch);
+  if (threadIdx.x == 0) {
+    lb[i] = l;
+    ub[i] = u;
+  }
+}
+
+// One wave: the candidates {i : LB_i <= min UB} in index order -> cand[1..], their count
+// -> cand[0]; -1 when a bound is NaN (the exact path runs), -2 when the count exceeds maxc;
+// cand[maxc + 1] = the row of the smallest UB (the next centre when the count is too large).
+__global__ void __launch_bounds__(64) krum_candidates(const double* __restrict__ lb,
+                                                      const double* __restrict__ ub, int64_t K,
+                                                      int64_t maxc, int64_t* __restrict__ cand) {
+  const int lane = threadIdx.x;
+  double m = __builtin_inf();
+  int64_t mi = K;
+  bool bad = false;
+  for (int64_t i = lane; i < K; i += 64) {
+    const double u = ub[i], l = lb[i];
+    bad |= u != u || l != l;
+    if (u < m) { m = u; mi = i; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double om = __shfl_xor(m, o);
+    const int64_t oi = __shfl_xor(mi, o);
+    if (om < m || (om == m && oi < mi)) { m = om; mi = oi; }
+  }
+  bad = __ballot(bad) != 0;
+  int64_t n = 0;
+  for (int64_t i0 = 0; i0 < K; i0 += 64) {
+    const int64_t i = i0 + lane;
+    const bool in = i < K && lb[i] <= m;
+    const uint64_t b = __ballot(in);
+    const int64_t pos = n + (int64_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+    if (in && pos < maxc) cand[1 + pos] = i;
+    n += __popcll(b);
+  }
+  if (lane == 0) {
+    cand[0] = (bad || n < 1) ? -1 : n > maxc ? -2 : n;
+    cand[maxc + 1] = mi < K ? mi : 0;
+  }
+}
+
+// The candidates' distance rows with pair_dist's arithmetic: slice blockIdx.y of the
+// columns (the exact path's krum_slices / chunk), 32-column stages, t = x_c - x_j (the
+// square of -t is the same bits), fp32 fma chain per stage, fp64 across stages.  A block
+// = 64 rows x up to kRefC candidates; per stage the rows go to LDS (coalesced: 8 lanes per
+// 128-byte row segment) and the candidates to LDS as interleaved PAIRS (c, c+1 of one
+// column adjacent), so one broadcast ds_read_b128 gives two columns of a candidate pair
+// and v_pk_add_f32 / v_pk_fma_f32 run the pair's two chains (per lane IEEE: the scalar
+// chain's bits).  Thread = (row jl, candidate-pair group grp): pairs grp, grp + 4, ...;
+// the next stage's loads in registers during this stage's arithmetic.  (Two rows per
+// thread — half the broadcast reads per FMA, half the blocks — measured slower: 2.40 vs
+// 1.77 ms without the prefetch.)
+// Measured against three register-heavy forms (each lane's rows straight from HBM, the
+// candidates by scalar loads, one wave per SIMD): 2.8 vs 4.4-5.8 ms at K = 256 x 4M.
+constexpr int kRefC = 32;
+template <bool VEC, int NPP>   // NPP: candidate pairs per thread (ceil(pairs / 4): no idle chains)
+__global__ void __launch_bounds__(256) krum_cand_dist(const float* __restrict__ X, int64_t K,
+                                                      int64_t d, int64_t ldx, int ws, int64_t chunk,
+                                                      const int64_t* __restrict__ cidx, int m,
+                                                      double* __restrict__ part) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  __shared__ __attribute__((aligned(16))) float sC[kRefC / 2][kPC * 2];   // [pair][col][2]
+  __shared__ float sR[64][kPC + 1];
+  const int tid = threadIdx.x, jl = tid & 63, grp = tid >> 6;
+  const int64_t j = (int64_t)blockIdx.x * 64 + jl;
+  const int64_t cb = (int64_t)blockIdx.y * chunk, ce = cb + chunk < d ? cb + chunk : d;
+  static_assert(NPP >= 1 && NPP <= kRefC / 8, "candidate pairs per thread");
+  double accd[NPP][2];
+#pragma unroll
+  for (int u = 0; u < NPP; ++u) accd[u][0] = accd[u][1] = 0.0;
+  auto ld4 = [&](int64_t row, int64_t col) {
+    f4 v = {0.f, 0.f, 0.f, 0.f};
+    if (col < ce) {
+      const float* src = elem(X, ldx, ws, row, col);
+      if (VEC && col + 4 <= ce) {
+        v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src));
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = col + u < ce ? src[u] : 0.f;
+      }
+    }
+    return v;
+  };
+  // stage loads in registers, the next stage's issued before this stage's arithmetic:
+  // rows (64 x 8 float4: two per thread), candidates (8 NPP x 8 float4: one per thread of
+  // the first 64 NPP; candidates >= m load zeros and are never stored)
+  const int cr = tid >> 3, ccg = (tid & 7) * 4;
+  const int64_t crow = tid < 64 * NPP && cr < m ? cidx[cr] : -1;
+  f4 pr[2], pc;
+  auto load_stage = [&](int64_t c0) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int idx = tid + 256 * q, r = idx >> 3, cg = (idx & 7) * 4;
+      const int64_t row = (int64_t)blockIdx.x * 64 + r;
+      pr[q] = row < K ? ld4(row, c0 + cg) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    pc = crow >= 0 ? ld4(crow, c0 + ccg) : f4{0.f, 0.f, 0.f, 0.f};
+  };
+  if (cb < ce) load_stage(cb);
+  for (int64_t c0 = cb; c0 < ce; c0 += kPC) {
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int idx = tid + 256 * q, r = idx >> 3, cg = (idx & 7) * 4;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sR[r][cg + u] = pr[q][u];
+    }
+    if (tid < 64 * NPP) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sC[cr >> 1][2 * (ccg + u) + (cr & 1)] = pc[u];
+    }
+    __syncthreads();
+    if (c0 + kPC < ce) load_stage(c0 + kPC);
+    f2 acc[NPP];
+#pragma unroll
+    for (int u = 0; u < NPP; ++u) acc[u] = f2{0.f, 0.f};
+#pragma unroll 4
+    for (int c = 0; c < kPC; c += 2) {
+      const float x0 = sR[jl][c], x1 = sR[jl][c + 1];
+#pragma unroll
+      for (int u = 0; u < NPP; ++u) {
+        const f4 cc = *reinterpret_cast<const f4*>(&sC[grp + 4 * u][2 * c]);
+        const f2 t0 = f2{cc[0], cc[1]} - f2{x0, x0};
+        acc[u] = __builtin_elementwise_fma(t0, t0, acc[u]);
+        const f2 t1 = f2{cc[2], cc[3]} - f2{x1, x1};
+        acc[u] = __builtin_elementwise_fma(t1, t1, acc[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NPP; ++u) {
+      accd[u][0] += (double)acc[u][0];
+      accd[u][1] += (double)acc[u][1];
+    }
+  }
+  if (j < K) {
+#pragma unroll
+    for (int u = 0; u < NPP; ++u)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int cc = 2 * (grp + 4 * u) + e;
+        if (cc < m) part[((int64_t)blockIdx.y * m + cc) * K + j] = accd[u][e];
+      }
+  }
+}
+
+// Dc[c][j] = the sum over slices in pair_reduce's order (4 waves split the slices,
+// ((w0 + w1) + w2) + w3).
+__global__ void __launch_bounds__(256) krum_cand_reduce(const double* __restrict__ part, int64_t S,
+                                                        int64_t n, double* __restrict__ Dc) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const bool on = e < n;
+  const int64_t s0 = S * w / 4, s1 = S * (w + 1) / 4;
+  double s = 0.0;
+  if (on) {
+#pragma unroll 8
+    for (int64_t t = s0; t < s1; ++t) s += part[t * n + e];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && on) Dc[e] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+// Candidate c's score from its distance row (krum_score's arithmetic).
+__global__ void __launch_bounds__(256) krum_cand_score(const double* __restrict__ Dc, int64_t K,
+                                                       int64_t kk, double* __restrict__ score) {
+  extern __shared__ double srow[];
+  __shared__ double scratch[8];
+  const int64_t c = blockIdx.x;
+  for (int64_t j = threadIdx.x; j < K; j += blockDim.x) srow[j] = Dc[c * K + j];
+  __syncthreads();
+  const double sc = krum_row_score(srow, K, kk, scratch);
+  if (threadIdx.x == 0) score[c] = sc;
+}
+
+// The first minimum over the candidates (ascending indices: krum_argmin's tie rule).
+__global__ void __launch_bounds__(64) krum_cand_argmin(const double* __restrict__ score,
+                                                       const int64_t* __restrict__ cidx, int64_t m,
+                                                       int64_t* __restrict__ index) {
+  int64_t best = -1;
+  double bv = 0.0;
+  for (int64_t q = threadIdx.x; q < m; q += 64)
+    if (best < 0 || score[q] < bv) { bv = score[q]; best = cidx[q]; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(bv, o);
+    const int64_t oi = __shfl_xor(best, o);
+    if (oi >= 0 && (best < 0 || ov < bv || (ov == bv && oi < best))) { bv = ov; best = oi; }
+  }
+  if (threadIdx.x == 0) *index = best;
+}
+
+// out = row k (k on the host)
+__global__ void __launch_bounds__(256) copy_row_k(const float* __restrict__ X, int64_t d,
+                                                  int64_t ldx, int ws, int64_t k,
+                                                  float* __restrict__ out) {
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < d;
        c += (int64_t)gridDim.x * blockDim.x)
     out[c] = *elem(X, ldx, ws, k, c);
@@ -1335,6 +1589,67 @@ int64_t krum_slices(int64_t K, int64_t d) {
     if (cost < best_cost * (1 - 1e-9)) { best_cost = cost; best = S; }
   }
   return best;
+}
+
+hipError_t launch_copy_row_k(const float* X, int64_t d, int64_t ldx, int ws, int64_t k, float* out,
+                             hipStream_t s) {
+  if (d > 0)
+    hipLaunchKernelGGL(copy_row_k, dim3((unsigned)std::min<int64_t>((d + 255) / 256, 2048)),
+                       dim3(256), 0, s, X, d, ldx, ws, k, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_krum_gram_select(const double* G, int KP, int64_t K, int64_t kk, double epsg,
+                                   double* lb, double* ub, int64_t maxc, int64_t* cand,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(krum_gram_bounds, dim3((unsigned)K), dim3(256), 2 * sizeof(double) * K, s, G,
+                     KP, K, kk, epsg, lb, ub);
+  hipLaunchKernelGGL(krum_candidates, dim3(1), dim3(64), 0, s, lb, ub, K, maxc, cand);
+  return hipGetLastError();
+}
+
+int krum_refine_max() { return kRefC; }
+
+hipError_t launch_krum_refine(const float* X, int64_t K, int64_t d, int64_t ldx, int ws,
+                              const int64_t* cidx, int m, int64_t kk, double* part, double* Dc,
+                              double* score, hipStream_t s) {
+  if (m < 1 || m > kRefC) return hipErrorInvalidValue;
+  const int64_t S = krum_slices(K, d);
+  const int64_t chunk = ((d + S - 1) / S + kPC - 1) / kPC * kPC;   // launch_krum's slices
+  const bool vec = reinterpret_cast<uintptr_t>(X) % 16 == 0 && ldx % 4 == 0;
+  const dim3 grid((unsigned)((K + 63) / 64), (unsigned)S);
+  const int npp = ((m + 1) / 2 + 3) / 4;                         // pairs per thread
+#define GMK_CAND(V_, N_)                                                                        \
+  hipLaunchKernelGGL((krum_cand_dist<V_, N_>), grid, dim3(256), 0, s, X, K, d, ldx, ws, chunk, cidx, \
+                     m, part)
+  if (vec) {
+    if (npp == 1) GMK_CAND(true, 1);
+    else if (npp == 2) GMK_CAND(true, 2);
+    else GMK_CAND(true, 4);
+  } else {
+    if (npp == 1) GMK_CAND(false, 1);
+    else if (npp == 2) GMK_CAND(false, 2);
+    else GMK_CAND(false, 4);
+  }
+#undef GMK_CAND
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int64_t n = (int64_t)m * K;
+  hipLaunchKernelGGL(krum_cand_reduce, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, part, S, n,
+                     Dc);
+  hipLaunchKernelGGL(krum_cand_score, dim3((unsigned)m), dim3(256), sizeof(double) * K, s, Dc, K, kk,
+                     score);
+  return hipGetLastError();
+}
+
+hipError_t launch_krum_pick(const double* score, const int64_t* cidx, int64_t m, const float* X,
+                            int64_t d, int64_t ldx, int ws, int64_t* index, float* out,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(krum_cand_argmin, dim3(1), dim3(64), 0, s, score, cidx, m, index);
+  if (d > 0)
+    hipLaunchKernelGGL(copy_row, dim3((unsigned)std::min<int64_t>((d + 255) / 256, 2048)),
+                       dim3(256), 0, s, X, d, ldx, ws, index, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t kk, double* D,

@@ -249,6 +249,22 @@ int64_t krum_slices(int64_t K, int64_t d);
 hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t kk, double* D,
                        double* part, double* score, float* out, int64_t* index, hipStream_t s,
                        int ws = 0);
+// Krum through the Gram (round 5): bounds + candidates from G [KP][KP] (lb, ub [K]; cand
+// [2 + maxc] int64: count, -1 (a bound not finite) or -2 (more than maxc), the indices, then
+// the row of the smallest upper bound), the candidates' exact rows (at most
+// krum_refine_max() per launch; part [krum_slices][m][K], Dc [m][K], score [m]), the pick.
+hipError_t launch_copy_row_k(const float* X, int64_t d, int64_t ldx, int ws, int64_t k, float* out,
+                             hipStream_t s);
+hipError_t launch_krum_gram_select(const double* G, int KP, int64_t K, int64_t kk, double epsg,
+                                   double* lb, double* ub, int64_t maxc, int64_t* cand,
+                                   hipStream_t s);
+int krum_refine_max();
+hipError_t launch_krum_refine(const float* X, int64_t K, int64_t d, int64_t ldx, int ws,
+                              const int64_t* cidx, int m, int64_t kk, double* part, double* Dc,
+                              double* score, hipStream_t s);
+hipError_t launch_krum_pick(const double* score, const int64_t* cidx, int64_t m, const float* X,
+                            int64_t d, int64_t ldx, int ws, int64_t* index, float* out,
+                            hipStream_t s);
 
 // The clients' local SGD chain of one federated step (clients.hip).
 struct ClientChainArgs {

@@ -226,6 +226,22 @@ int gm_trimmed_mean_panels_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d
 int gm_krum_panels_f32(gm_ctx* ctx, const float* X, int64_t K, int64_t d, int64_t panel_stride,
                        int64_t honest_size, float* out, int64_t* index, void* stream);
 
+/* Krum's algorithm (round 5).  K <= 256 on large inputs (AUTO: K >= 64 and K^2 d >= 2^29;
+ * env GMAGG_KRUM=0 exact only, 1 Gram wherever eligible): the scaled-f16 Gram MFMA kernel
+ * gives every pairwise distance within a stated bound, rows whose score bounds reach the
+ * smallest upper bound are recomputed with the exact path's arithmetic, and the index equals
+ * the exact path's.  gm_krum_last_info: info[3] = {algorithm, candidates recomputed,
+ * reason} of this context's last Krum call. */
+enum gm_krum_algo { GM_KRUM_EXACT = 0, GM_KRUM_GRAM = 1 };
+enum gm_krum_reason {
+  GM_KRUM_REASON_OK = 0,             /* the Gram path ran */
+  GM_KRUM_REASON_NOT_CHOSEN = 1,     /* exact by choice (GMAGG_KRUM, AUTO's size rule) */
+  GM_KRUM_REASON_NOT_ELIGIBLE = 2,   /* K > 256, misaligned rows, d or ldx % 4, panel width */
+  GM_KRUM_REASON_GRAM_NONFINITE = 3, /* the f16 range was exceeded or the input is not finite */
+  GM_KRUM_REASON_CANDIDATES = 4      /* more than 128 candidates, or a bound not finite */
+};
+int gm_krum_last_info(gm_ctx* ctx, int64_t* info);
+
 /* getVarience(w_local, honestSize) (MNIST_Air_weight.py:127-129): the mean over the
  * first `honest` rows of ||x_k - mean||^2, written as ONE fp32 value to the device
  * pointer `out`; one streaming pass over the honest rows (fp64 sums). */

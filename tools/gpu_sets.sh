@@ -287,6 +287,19 @@ for k in sorted(acc):
 PY
 }
 
+krum() {
+  # Round 5: Krum through the Gram MFMA kernel against the exact pair-distance path over
+  # (K, d), then the kernel trace of both paths at K = 256 x 4M
+  timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_krum_gram.py \
+    > $O/t.log 2>&1 || { tail -30 $O/t.log; return 3; }
+  tail -1 $O/t.log
+  timeout -k 10 600 python -u tools/krum_bench.py --reps 5 > $O/krum.jsonl 2> $O/krum.err || { tail -20 $O/krum.err; return 1; }
+  cat $O/krum.jsonl
+  GMAGG_KRUM=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o t -- \
+    python3 tools/krum_bench.py --shapes 256x4194304 --reps 5 > $O/trace.log 2>&1 || return 2
+  cut -c1-150 $O/trace/t_kernel_stats.csv | head -14
+}
+
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 O=gpurun_out/${2:-$1}
 mkdir -p "$O"
