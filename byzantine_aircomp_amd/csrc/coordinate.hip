@@ -1026,6 +1026,109 @@ __global__ void __launch_bounds__(C * 64, 2) col_select1(const float* __restrict
   if (lane == 0) out[j0 + w] = res[0];
 }
 
+// Staged-transpose selection (round 5): the column tile never sits in LDS whole.  A block
+// of NWV waves owns C = NWV x NC columns (C = 16: 64-byte row segments, adjacent tiles on
+// one XCD as col_select1); 256-row rounds go HBM -> registers -> a 17-KB LDS stage -> each
+// wave's NC columns as keys in registers, so LDS no longer caps the columns in flight per
+// CU (col_select: two 69.6-KB tiles = 32 columns) and the VGPRs do: NC chains per wave.
+// The compaction slots are per chain (scr), contiguous.
+#ifndef GMK_SELECT_ST_PREFETCH
+#define GMK_SELECT_ST_PREFETCH 0   // A/B: the next staging round's loads in flight
+#endif
+#ifndef GMK_SELECT_ST_WPE
+#define GMK_SELECT_ST_WPE 0   // A/B: minimum waves per SIMD the compiler must fit (0: its choice)
+#endif
+#if GMK_SELECT_ST_WPE
+#define GMK_ST_ATTR __attribute__((amdgpu_waves_per_eu(GMK_SELECT_ST_WPE, 8)))
+#else
+#define GMK_ST_ATTR
+#endif
+template <int MODE, int R, int NC, int NWV>
+__global__ void __launch_bounds__(NWV * 64) GMK_ST_ATTR col_select_st(const float* __restrict__ X, int64_t K,
+                                                         int64_t d, int64_t ldx, int ws, int64_t b,
+                                                         int vec4, float* __restrict__ out) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int C = NWV * NC;
+  static_assert(C == 16, "64-byte row segments");
+  constexpr int SR = 256;                          // rows per staging round
+  constexpr int NRD = (64 * R + SR - 1) / SR;      // rounds
+  constexpr int R2 = R >= 4 ? 2 : 0;
+  constexpr int SLOTS = MODE == 0 ? 64 * (R2 > 0 ? R2 : 1) : 512;
+  constexpr int LPR = C / 4, RPI = NWV * 64 / LPR, NLD = SR / RPI;
+  static_assert(SR % RPI == 0 && SR % 64 == 0 && (64 * R) % SR == 0, "round shape");
+  __shared__ float stage[SR][C + 1];
+  __shared__ uint32_t scr[NWV][NC][SLOTS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tq = threadIdx.x % LPR, tr = threadIdx.x / LPR;
+  const int64_t ntiles = (d + C - 1) / C;
+  const int64_t v = blockIdx.x;
+  if (v >= ntiles) return;
+  // blocks bid and bid + 8 share an XCD: adjacent tiles, one 128-B line's two halves
+  const int64_t t = (v < ntiles / 16 * 16) ? v / 16 * 16 + (v % 8) * 2 + (v / 8) % 2 : v;
+  const int64_t j0 = t * C;
+  const int64_t col = j0 + 4 * tq;
+  const bool vec = vec4 && col + 4 <= d;
+  uint32_t key[NC][R];
+  bool nan[NC];
+#pragma unroll
+  for (int h = 0; h < NC; ++h) nan[h] = false;
+  // round rd + 1's loads are issued before round rd's staging (GMK_SELECT_ST_PREFETCH)
+  f4 buf[GMK_SELECT_ST_PREFETCH ? 2 : 1][NLD];
+  auto load = [&](int rd, f4 (&dst)[NLD]) {
+#pragma unroll
+    for (int u = 0; u < NLD; ++u) {
+      const int64_t k = rd * SR + tr + (int64_t)u * RPI;
+      dst[u] = f4{0.f, 0.f, 0.f, 0.f};
+      if (k < K) {
+        const float* src = elem(X, ldx, ws, k, col);
+        if (vec) {
+          dst[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dst[u][e] = col + e < d ? src[e] : 0.f;
+        }
+      }
+    }
+  };
+  if constexpr (GMK_SELECT_ST_PREFETCH) load(0, buf[0]);
+#pragma unroll
+  for (int rd = 0; rd < NRD; ++rd) {
+    constexpr int P = GMK_SELECT_ST_PREFETCH ? 1 : 0;
+    f4 (&cur)[NLD] = buf[P ? (rd & 1) : 0];
+    if constexpr (P) {
+      if (rd + 1 < NRD) load(rd + 1, buf[(rd + 1) & 1]);
+    } else {
+      load(rd, cur);
+    }
+    if (rd > 0) __syncthreads();                   // the previous round's reads are done
+#pragma unroll
+    for (int u = 0; u < NLD; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) stage[tr + u * RPI][4 * tq + e] = cur[u][e];
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < NC; ++h) {
+      const int64_t c = j0 + w * NC + h;
+#pragma unroll
+      for (int i = 0; i < SR / 64; ++i) {
+        const int64_t row = rd * SR + lane + 64 * i;
+        const bool ok = row < K && c < d;
+        const float x = ok ? stage[lane + 64 * i][w * NC + h] : 0.f;
+        key[h][rd * (SR / 64) + i] = ok ? order_key(x) : 0xFFFFFFFFu;
+        nan[h] |= ok && x != x;
+      }
+    }
+  }
+  auto bufc = [&](int h, int q) { return &scr[w][h][q * 64 * (R2 > 0 ? R2 : 1)]; };
+  float res[NC];
+  select_pair<MODE, R, R2, 1, NC>(key, nan, K, b, bufc, res);
+  if (lane == 0) {
+#pragma unroll
+    for (int h = 0; h < NC; ++h)
+      if (j0 + w * NC + h < d) out[j0 + w * NC + h] = res[h];
+  }
+}
+
 // Krum, step 1: squared distances of every row pair, register-tiled.
 // A block owns a 128 x 128 tile of pairs (row tiles bi <= bj: D is symmetric)
 // over one slice of the columns; each of 512 threads an 8 x 4 sub-tile (8 x 8 with
@@ -1540,6 +1643,34 @@ hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, 
     return e ? atoi(e) : -1;
   }();
   const bool one_col = one_col_env < 0 ? mode == 1 : one_col_env != 0;
+  // The median at 128 < K <= 1024 on the staged-transpose kernel (col_select_st: two
+  // columns per wave, 8 waves, the tile never whole in LDS): x 2M columns, K = 200 / 256 /
+  // 400 / 1000: 1.15 / 1.20 / 1.81 / 3.78 -> 1.01 / 1.05 / 1.42 / 3.19 ms; at K = 2000
+  // (R = 32: 166 VGPRs) slower, 12.85 vs 12.17 (profiles/r5s2_select_st_ab.jsonl).  The
+  // trimmed mean measured slower on it (4.92 vs 4.37 ms at K = 1000 on col_select1), four
+  // columns per wave slower for both, forced 7 / 8 waves per SIMD (spills) slower too.
+  // GMAGG_SELECT_ST: 0 never, 1 the median (default), 2 both modes (A/B).
+  static const int st_env = [] {
+    const char* e = getenv("GMAGG_SELECT_ST");
+    return e ? atoi(e) : 1;
+  }();
+  if ((st_env == 2 || (st_env == 1 && mode == 0)) && K > 128 && K <= 1024) {
+    const dim3 g((unsigned)((d + 15) / 16));
+#define GMK_ST(R_)                                                                              \
+  do {                                                                                          \
+    if (mode == 0)                                                                              \
+      hipLaunchKernelGGL((col_select_st<0, R_, 2, 8>), g, dim3(512), 0, s, X, K, d, ldx, ws, b,   \
+                         vec4, out);                                                            \
+    else                                                                                        \
+      hipLaunchKernelGGL((col_select_st<1, R_, 2, 8>), g, dim3(512), 0, s, X, K, d, ldx, ws, b,   \
+                         vec4, out);                                                            \
+  } while (0)
+    if (K <= 256) GMK_ST(4);
+    else if (K <= 512) GMK_ST(8);
+    else GMK_ST(16);
+#undef GMK_ST
+    return hipGetLastError();
+  }
   if (K <= 64) GMK_SEL(1, 32, 4);
   else if (K <= 128) GMK_SEL(2, 32, 4);
   // at 128 < K <= 256 the other way round: the median gains on one column per wave (1.34 ->

@@ -300,6 +300,78 @@ krum() {
   cut -c1-150 $O/trace/t_kernel_stats.csv | head -14
 }
 
+st_ab() {
+  # Round 5: the staged-transpose selection kernel (GMAGG_SELECT_ST=1: the median, default;
+  # 2: both modes; 0: the round-4 tiles): the f3 tests under each, then select_bench
+  # interleaved over K
+  for v in 0 2; do
+    GMAGG_SELECT_ST=$v timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+      tests/test_gpu_other_aggregators.py > $O/t$v.log 2>&1 || { tail -30 $O/t$v.log; return 1; }
+    tail -1 $O/t$v.log
+  done
+  for r in 1 2 3; do
+    for v in 0 1; do
+      GMAGG_SELECT_ST=$v timeout -k 10 200 python -u tools/select_bench.py --K 2000 1000 400 256 200 --reps 5 \
+        | sed "s/}$/, \"st\": $v}/" >> $O/sel.jsonl || return 2
+    done
+  done
+  python3 - "$O" <<'PY'
+import collections, json, sys
+acc = collections.defaultdict(list)
+for l in open(sys.argv[1] + "/sel.jsonl"):
+    r = json.loads(l)
+    acc[(r["agg"], r["K"], r["st"])].append(r["ms"])
+for k in sorted(acc):
+    print(k, " ".join(f"{v:.3f}" for v in acc[k]))
+PY
+}
+
+st_wpe() {
+  # the staged-transpose median (GMAGG_SELECT_ST=2) at the compiler's occupancy (6 waves per
+  # SIMD) against forced 7 / 8 (libgmagg_wpeN.so: make alt ALT_ONLY=coordinate
+  # ALT_FLAGS=-DGMK_SELECT_ST_WPE=N)
+  for r in 1 2 3; do
+    for v in "st0:GMAGG_SELECT_ST=0" "st2:GMAGG_SELECT_ST=2" \
+             "wpe7:GMAGG_SELECT_ST=2 GMAGG_LIB=byzantine_aircomp_amd/libgmagg_wpe7.so" \
+             "wpe8:GMAGG_SELECT_ST=2 GMAGG_LIB=byzantine_aircomp_amd/libgmagg_wpe8.so"; do
+      n=${v%%:*}; e=${v#*:}
+      env $e timeout -k 10 120 python -u tools/select_bench.py --K 1000 --reps 5 \
+        | sed "s/}$/, \"v\": \"$n\"}/" >> $O/sel.jsonl || return 2
+    done
+  done
+  python3 - "$O" <<'PY'
+import collections, json, sys
+acc = collections.defaultdict(list)
+for l in open(sys.argv[1] + "/sel.jsonl"):
+    r = json.loads(l)
+    acc[(r["agg"], r["K"], r["v"])].append(r["ms"])
+for k in sorted(acc):
+    print(k, " ".join(f"{v:.3f}" for v in acc[k]))
+PY
+}
+
+st_pf() {
+  # the staged median with the next round's loads in flight (libgmagg_alt.so: make alt
+  # ALT_ONLY=coordinate ALT_FLAGS=-DGMK_SELECT_ST_PREFETCH=1) against the default
+  for r in 1 2 3; do
+    for v in "def:" "pf:GMAGG_LIB=byzantine_aircomp_amd/libgmagg_alt.so"; do
+      n=${v%%:*}; e=${v#*:}
+      env $e timeout -k 10 120 python -u tools/select_bench.py --K 1000 400 256 --reps 5 \
+        | sed "s/}$/, \"v\": \"$n\"}/" >> $O/sel.jsonl || return 2
+    done
+  done
+  python3 - "$O" <<'PY'
+import collections, json, sys
+acc = collections.defaultdict(list)
+for l in open(sys.argv[1] + "/sel.jsonl"):
+    r = json.loads(l)
+    if r["agg"] == "median":
+        acc[(r["agg"], r["K"], r["v"])].append(r["ms"])
+for k in sorted(acc):
+    print(k, " ".join(f"{v:.3f}" for v in acc[k]))
+PY
+}
+
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 O=gpurun_out/${2:-$1}
 mkdir -p "$O"
