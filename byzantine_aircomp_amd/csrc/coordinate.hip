@@ -167,6 +167,18 @@ __device__ __forceinline__ uint32_t order_key(float x) {
   if (x == 0.f) u = 0u;
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
+// The key of a held slot (round 5: 4-6 VALU, no branch; the LDS read before it is
+// unconditional — padding rows hold finite garbage or zeros — so a wave's reads issue back
+// to back): ok = false (a row past K, a column past d) -> 0xFFFFFFFF; -0 as +0 (x + 0);
+// NaN -> 0xFFFFFFFF (above +inf: torch's order for topk) when NANTOP, else whatever key
+// its bits give (the median returns NaN for a column holding one, select_pair).
+template <bool NANTOP>
+__device__ __forceinline__ uint32_t slot_key(float x, bool ok) {
+  const uint32_t u = __float_as_uint(x + 0.0f);
+  uint32_t k = u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
+  if constexpr (NANTOP) k = x != x ? 0xFFFFFFFFu : k;
+  return ok ? k : 0xFFFFFFFFu;
+}
 __device__ __forceinline__ float key_value(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
@@ -864,9 +876,9 @@ __device__ __forceinline__ void select_tile(float (&tile)[64 * R][C + 1], int64_
 #pragma unroll
       for (int i = 0; i < R; ++i) {
         const int row = lane + 64 * i;
-        const bool ok = row < K && j0 + c0 + NWV * h < d;
-        const float x = ok ? tile[row][c0 + NWV * h] : 0.f;
-        key[h][i] = ok ? order_key(x) : 0xFFFFFFFFu;
+        const bool ok = row < (int)K && j0 + c0 + NWV * h < d;
+        const float x = tile[row][c0 + NWV * h];
+        key[h][i] = slot_key<MODE == 1>(x, ok);
         nan[h] |= ok && x != x;
       }
     float res[2];
@@ -1012,9 +1024,9 @@ __global__ void __launch_bounds__(C * 64, 2) col_select1(const float* __restrict
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int row = lane + 64 * i;
-    const bool ok = row < K;
-    const float x = ok ? tile[row][w] : 0.f;
-    key[0][i] = ok ? order_key(x) : 0xFFFFFFFFu;
+    const bool ok = row < (int)K;
+    const float x = tile[row][w];
+    key[0][i] = slot_key<MODE == 1>(x, ok);
     nan[0] |= ok && x != x;
   }
   constexpr int R2 = R >= 4 ? 2 : 0;
@@ -1073,8 +1085,22 @@ __global__ void __launch_bounds__(NWV * 64) GMK_ST_ATTR col_select_st(const floa
 #pragma unroll
   for (int h = 0; h < NC; ++h) nan[h] = false;
   // round rd + 1's loads are issued before round rd's staging (GMK_SELECT_ST_PREFETCH)
-  f4 buf[GMK_SELECT_ST_PREFETCH ? 2 : 1][NLD];
+  f4 buf[GMK_SELECT_ST_PREFETCH == 1 ? 2 : 1][NLD];
+  // a whole in-range, aligned tile (wave-uniform): every load issued unconditionally from a
+  // clamped row, rows past K zeroed after, so the loads go out back to back (a per-load
+  // branch made the compiler wait for each); the edge tile takes the guarded path
+  const bool vec_tile = vec4 && j0 + C <= d;
   auto load = [&](int rd, f4 (&dst)[NLD]) {
+    if (vec_tile) {
+#pragma unroll
+      for (int u = 0; u < NLD; ++u) {
+        const int k = rd * SR + tr + u * RPI;
+        const f4 x = __builtin_nontemporal_load(
+            reinterpret_cast<const f4*>(elem(X, ldx, ws, k < (int)K ? k : (int)K - 1, col)));
+        dst[u] = k < (int)K ? x : f4{0.f, 0.f, 0.f, 0.f};
+      }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < NLD; ++u) {
       const int64_t k = rd * SR + tr + (int64_t)u * RPI;
@@ -1090,14 +1116,22 @@ __global__ void __launch_bounds__(NWV * 64) GMK_ST_ATTR col_select_st(const floa
       }
     }
   };
-  if constexpr (GMK_SELECT_ST_PREFETCH) load(0, buf[0]);
+  // GMK_SELECT_ST_PREFETCH = 2: every round's loads issued up front (NRD x NLD float4)
+  f4 all[GMK_SELECT_ST_PREFETCH == 2 ? NRD : 1][NLD];
+  if constexpr (GMK_SELECT_ST_PREFETCH == 2) {
+#pragma unroll
+    for (int rd = 0; rd < NRD; ++rd) load(rd, all[rd]);
+  } else if constexpr (GMK_SELECT_ST_PREFETCH == 1) {
+    load(0, buf[0]);
+  }
 #pragma unroll
   for (int rd = 0; rd < NRD; ++rd) {
-    constexpr int P = GMK_SELECT_ST_PREFETCH ? 1 : 0;
-    f4 (&cur)[NLD] = buf[P ? (rd & 1) : 0];
-    if constexpr (P) {
+    constexpr int P = GMK_SELECT_ST_PREFETCH == 1 ? 1 : 0;
+    f4 (&cur)[NLD] = GMK_SELECT_ST_PREFETCH == 2 ? all[GMK_SELECT_ST_PREFETCH == 2 ? rd : 0]
+                                                  : buf[P ? (rd & 1) : 0];
+    if constexpr (GMK_SELECT_ST_PREFETCH == 1) {
       if (rd + 1 < NRD) load(rd + 1, buf[(rd + 1) & 1]);
-    } else {
+    } else if constexpr (GMK_SELECT_ST_PREFETCH == 0) {
       load(rd, cur);
     }
     if (rd > 0) __syncthreads();                   // the previous round's reads are done
@@ -1108,13 +1142,13 @@ __global__ void __launch_bounds__(NWV * 64) GMK_ST_ATTR col_select_st(const floa
     __syncthreads();
 #pragma unroll
     for (int h = 0; h < NC; ++h) {
-      const int64_t c = j0 + w * NC + h;
+      const bool cok = j0 + w * NC + h < d;       // wave-uniform
 #pragma unroll
       for (int i = 0; i < SR / 64; ++i) {
-        const int64_t row = rd * SR + lane + 64 * i;
-        const bool ok = row < K && c < d;
-        const float x = ok ? stage[lane + 64 * i][w * NC + h] : 0.f;
-        key[h][rd * (SR / 64) + i] = ok ? order_key(x) : 0xFFFFFFFFu;
+        const int row = rd * SR + lane + 64 * i;
+        const bool ok = cok && row < (int)K;
+        const float x = stage[lane + 64 * i][w * NC + h];
+        key[h][rd * (SR / 64) + i] = slot_key<MODE == 1>(x, ok);
         nan[h] |= ok && x != x;
       }
     }

@@ -372,6 +372,30 @@ for k in sorted(acc):
 PY
 }
 
+sel_keys() {
+  # this build's selection kernels against the previous build (libgmagg_old.so, copied
+  # aside); the f3 tests first
+  timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+    tests/test_gpu_other_aggregators.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  for r in 1 2 3; do
+    for v in "new:" "old:GMAGG_LIB=byzantine_aircomp_amd/libgmagg_old.so"; do
+      n=${v%%:*}; e=${v#*:}
+      env $e timeout -k 10 200 python -u tools/select_bench.py --K 1000 400 256 --reps 5 \
+        | sed "s/}$/, \"v\": \"$n\"}/" >> $O/sel.jsonl || return 2
+    done
+  done
+  python3 - "$O" <<'PY'
+import collections, json, sys
+acc = collections.defaultdict(list)
+for l in open(sys.argv[1] + "/sel.jsonl"):
+    r = json.loads(l)
+    acc[(r["agg"], r["K"], r["v"])].append(r["ms"])
+for k in sorted(acc):
+    print(k, " ".join(f"{v:.3f}" for v in acc[k]))
+PY
+}
+
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 O=gpurun_out/${2:-$1}
 mkdir -p "$O"
