@@ -1681,14 +1681,16 @@ hipError_t launch_col_select(const float* X, int64_t K, int64_t d, int64_t ldx, 
   // columns per wave, 8 waves, the tile never whole in LDS): x 2M columns, K = 200 / 256 /
   // 400 / 1000: 1.15 / 1.20 / 1.81 / 3.78 -> 1.01 / 1.05 / 1.42 / 3.19 ms; at K = 2000
   // (R = 32: 166 VGPRs) slower, 12.85 vs 12.17 (profiles/r5s2_select_st_ab.jsonl).  The
-  // trimmed mean measured slower on it (4.92 vs 4.37 ms at K = 1000 on col_select1), four
-  // columns per wave slower for both, forced 7 / 8 waves per SIMD (spills) slower too.
-  // GMAGG_SELECT_ST: 0 never, 1 the median (default), 2 both modes (A/B).
+  // trimmed mean gains on it at K <= 512 (K = 256 / 400: 2.09 / 3.15 -> 1.95 / 2.99 ms) and
+  // loses at K = 1000 (4.52 vs 4.22 on col_select1; profiles/r5s3_select_st_tm_ab.jsonl);
+  // four columns per wave slower for both, forced 7 / 8 waves per SIMD (spills) slower too.
+  // GMAGG_SELECT_ST: 0 never, 1 (default) the median to K = 1024 and the trimmed mean to
+  // K = 512, 2 both to K = 1024 (A/B).
   static const int st_env = [] {
     const char* e = getenv("GMAGG_SELECT_ST");
     return e ? atoi(e) : 1;
   }();
-  if ((st_env == 2 || (st_env == 1 && mode == 0)) && K > 128 && K <= 1024) {
+  if (K > 128 && (st_env == 2 ? K <= 1024 : st_env == 1 && K <= (mode == 0 ? 1024 : 512))) {
     const dim3 g((unsigned)((d + 15) / 16));
 #define GMK_ST(R_)                                                                              \
   do {                                                                                          \

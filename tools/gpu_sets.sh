@@ -396,6 +396,25 @@ for k in sorted(acc):
 PY
 }
 
+st_tm() {
+  # the trimmed mean on the staged kernel (GMAGG_SELECT_ST=2) against col_select1 (default)
+  for r in 1 2 3; do
+    for v in 1 2; do
+      GMAGG_SELECT_ST=$v timeout -k 10 200 python -u tools/select_bench.py --K 1000 400 256 --reps 5 \
+        | sed "s/}$/, \"st\": $v}/" >> $O/sel.jsonl || return 2
+    done
+  done
+  python3 - "$O" <<'PY'
+import collections, json, sys
+acc = collections.defaultdict(list)
+for l in open(sys.argv[1] + "/sel.jsonl"):
+    r = json.loads(l)
+    acc[(r["agg"], r["K"], r["st"])].append(r["ms"])
+for k in sorted(acc):
+    print(k, " ".join(f"{v:.3f}" for v in acc[k]))
+PY
+}
+
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 O=gpurun_out/${2:-$1}
 mkdir -p "$O"
