@@ -130,3 +130,27 @@ def test_gram_krum_auto_choice(monkeypatch):
         X = _recipe(K, d, int(0.8 * K), K + d, perm=False).cuda()
         bz.Krum(X, {"honestSize": int(0.8 * K)})
         assert bz.aggregators.Krum.last_info["algo"] == want, (K, d)
+
+
+@pytest.mark.parametrize("K,d", [(64, 4), (70, 60), (96, 1028), (255, 3000)])
+def test_gram_krum_small_and_ragged(K, d, monkeypatch):
+    """One Gram stage or less (d = 4, 60), a column count off the 64-column stage, K just
+    under the 256-row tile: still the exact path's row."""
+    X = _recipe(K, d, int(0.8 * K), 3 * K + d).cuda()
+    a, ia, info, b, ib = _both(X, int(0.8 * K), monkeypatch)
+    assert info["algo"] == "gram" or info["reason"] == "candidates", info
+    assert ia == ib and torch.equal(a, b)
+
+
+def test_gram_krum_panels_ragged(monkeypatch):
+    """Panels whose last panel is partial (d = 1000 at W = 64)."""
+    import byzantine_aircomp_amd as bz
+    X = _recipe(200, 1000, 160, 21).cuda()
+    P = bz.ClientPanels.from_rows(X)
+    monkeypatch.setenv("GMAGG_KRUM", "1")
+    a = bz.Krum(P, {"honestSize": 160})
+    ia, info = bz.aggregators.Krum.last_index, dict(bz.aggregators.Krum.last_info)
+    monkeypatch.setenv("GMAGG_KRUM", "0")
+    b = bz.Krum(X, {"honestSize": 160})
+    assert info["algo"] == "gram" or info["reason"] == "candidates", info
+    assert bz.aggregators.Krum.last_index == ia and torch.equal(a, b)
