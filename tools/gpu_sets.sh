@@ -46,7 +46,7 @@ pmc() {
   # HBM traffic of the dominant kernels (one counter per pass; tools/pmc_summary.py applies
   # the gfx950 FETCH_SIZE correction): C3 panels, C4 whole job, C5 both readings
   for w in "c3:" "c4:--workload c4 --steps 2 --warmup 1" "c5:--workload c5 --steps 1 --warmup 0" \
-           "c5air:--workload c5 --reading aircomp --steps 1 --warmup 0"; do
+           "c5air:--workload c5 --reading aircomp --steps 1 --warmup 0" "c2:--workload c2 --steps 3 --warmup 1"; do
     n=${w%%:*}; a=${w#*:}
     for c in FETCH_SIZE WRITE_SIZE; do
       timeout -s KILL 400 rocprofv3 --pmc $c --output-format csv -d $O/pmc_${n}_$c -o p -- \
