@@ -874,6 +874,15 @@ bool resident_plan(const PassCfg& cfg, int64_t nch, int num_cu, int* cpb_out, in
       cpb = c;
       if ((nch + c - 1) / c <= kResTargetBlocks) break;
     }
+    // beyond one XCD in the hierarchical gather's range (>= 90 blocks of the largest
+    // tile): half the columns per block, twice the blocks (up to 192), measured faster —
+    // 50 x 48,670 (V = 2) 96 -> 191 blocks 7.6 -> 7.0 us per iteration, 40 / 64 x 48,670
+    // likewise, 50 x 48,671 (V = 1) 7.8 -> 7.3; at 40-80 blocks the larger blocks stay
+    // ahead (50 x 20,001: 6.7 vs 7.2; profiles/r5s3_resident_cpb_*ab.jsonl)
+    const int64_t nb0 = cpb ? (nch + cpb - 1) / cpb : 0;
+    if (cpb >= 2 && nb0 > kResTargetBlocks && nb0 >= 90 &&
+        (nch + cpb / 2 - 1) / (cpb / 2) <= 192 && resident_kernel(cfg, cpb / 2))
+      cpb /= 2;
   }
   if (cpb == 0) return false;
   const void* fn = resident_kernel(cfg, cpb);

@@ -104,7 +104,8 @@ def test_split_scope_equals_flat(K, d, monkeypatch):
 
 def test_hier_default_choice():
     """AUTO takes the hierarchical gather where it measured faster (>= 90 blocks at
-    K > 32: the EMNIST MLP's 50 x 48,670, 96 blocks) and the split-scope one-hop exchange on
+    K > 32: the EMNIST MLP's 50 x 48,670, 191 blocks of 256 columns since round 5's block
+    rule, 96 of 512 before) and the split-scope one-hop exchange on
     the other grids beyond one XCD (50 x 20,000: 40 blocks); both exist for the 8-wave tile
     (32 < K <= 64) only, so K = 10 gathers flat (profiles/r5s1_resident_*_ab.jsonl)."""
     import byzantine_aircomp_amd as bz

@@ -415,6 +415,70 @@ for k in sorted(acc):
 PY
 }
 
+cpb_ab() {
+  # Round 5: the resident kernel beyond one XCD at smaller blocks (GMAGG_RES_CPB = chunks of
+  # 128 columns per block: 4 is AUTO's choice at d = 48,670 -> 96 blocks; 2 -> 191, 1 -> 381)
+  # under each gather
+  for r in 1 2; do
+    for cpb in 4 2 1; do
+      for ex in "auto:GMAGG_RES_HIER=1" "split:GMAGG_RES_HIER=0" "flat:GMAGG_RES_HIER=0 GMAGG_RES_SPLIT=0"; do
+        n=${ex%%:*}; e=${ex#*:}
+        env GMAGG_RES_CPB=$cpb $e timeout -k 10 200 python -u tools/res_shape_bench.py --shapes 50x48670,50x30000 --reps 5 \
+          | sed "s/}$/, \"cpb\": $cpb, \"ex\": \"$n\"}/" >> $O/cpb.jsonl || return 3
+      done
+    done
+  done
+  python3 - "$O" <<'PY'
+import collections, json, sys
+acc = collections.defaultdict(list)
+for l in open(sys.argv[1] + "/cpb.jsonl"):
+    r = json.loads(l)
+    acc[(r["K"], r["d"], r["cpb"], r["ex"], r["exchange"], r["algo"])].append(r["us_per_iteration"])
+for k in sorted(acc):
+    print(k, " ".join(f"{v:.2f}" for v in acc[k]))
+PY
+}
+
+cpb_ab2() {
+  # the resident kernel's block size beyond one XCD under AUTO's exchange: 4 chunks per
+  # block (AUTO's current choice, the fewest blocks) against 2, over shapes
+  for r in 1 2; do
+    for cpb in 4 2; do
+      GMAGG_RES_CPB=$cpb timeout -k 10 300 python -u tools/res_shape_bench.py \
+        --shapes 50x20000,50x40000,50x48670,50x60000,40x48670,64x48670,64x30000 --reps 5 \
+        | sed "s/}$/, \"cpb\": $cpb}/" >> $O/cpb.jsonl || return 3
+    done
+  done
+  python3 - "$O" <<'PY'
+import collections, json, sys
+acc = collections.defaultdict(list)
+for l in open(sys.argv[1] + "/cpb.jsonl"):
+    r = json.loads(l)
+    acc[(r["K"], r["d"], r["cpb"], r["exchange"], r["algo"])].append(r["us_per_iteration"])
+for k in sorted(acc):
+    print(k, " ".join(f"{v:.2f}" for v in acc[k]))
+PY
+}
+
+cpb_ab3() {
+  # odd d (the 1-value tile, V = 1): 8 chunks per block (AUTO's largest valid) against 4 and 2
+  for r in 1 2; do
+    for cpb in 8 4 2; do
+      GMAGG_RES_CPB=$cpb timeout -k 10 300 python -u tools/res_shape_bench.py \
+        --shapes 50x48671,50x30001,50x20001 --reps 5 | sed "s/}$/, \"cpb\": $cpb}/" >> $O/cpb.jsonl || return 3
+    done
+  done
+  python3 - "$O" <<'PY'
+import collections, json, sys
+acc = collections.defaultdict(list)
+for l in open(sys.argv[1] + "/cpb.jsonl"):
+    r = json.loads(l)
+    acc[(r["K"], r["d"], r["cpb"], r["exchange"], r["algo"])].append(r["us_per_iteration"])
+for k in sorted(acc):
+    print(k, " ".join(f"{v:.2f}" for v in acc[k]))
+PY
+}
+
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 O=gpurun_out/${2:-$1}
 mkdir -p "$O"
