@@ -878,9 +878,17 @@ bool resident_plan(const PassCfg& cfg, int64_t nch, int num_cu, int* cpb_out, in
     // tile): half the columns per block, twice the blocks (up to 192), measured faster —
     // 50 x 48,670 (V = 2) 96 -> 191 blocks 7.6 -> 7.0 us per iteration, 40 / 64 x 48,670
     // likewise, 50 x 48,671 (V = 1) 7.8 -> 7.3; at 40-80 blocks the larger blocks stay
-    // ahead (50 x 20,001: 6.7 vs 7.2; profiles/r5s3_resident_cpb_*ab.jsonl)
+    // ahead (50 x 20,001: 6.7 vs 7.2; profiles/r5s3_resident_cpb_*ab.jsonl).  The 8-wave
+    // tile only (32 < K <= 64, the one with the hierarchical gather): the flat gather of
+    // the K <= 32 tiles ran slower on smaller blocks (20 / 30 x 48,670: 6.4 / 6.6 -> 7.3 /
+    // 7.6; profiles/r5s3_resident_halve_ab.jsonl)
+    static const bool halve = [] {           // GMAGG_RES_HALVE=0: the largest tile (A/B)
+      const char* e = getenv("GMAGG_RES_HALVE");
+      return !e || atoi(e) != 0;
+    }();
     const int64_t nb0 = cpb ? (nch + cpb - 1) / cpb : 0;
-    if (cpb >= 2 && nb0 > kResTargetBlocks && nb0 >= 90 &&
+    const bool hier_tile = cfg.NW == 8 && cfg.LPR == 64 && cfg.R == 8;   // 32 < K <= 64
+    if (halve && hier_tile && cpb >= 2 && nb0 > kResTargetBlocks && nb0 >= 90 &&
         (nch + cpb / 2 - 1) / (cpb / 2) <= 192 && resident_kernel(cfg, cpb / 2))
       cpb /= 2;
   }

@@ -479,6 +479,27 @@ for k in sorted(acc):
 PY
 }
 
+halve_ab() {
+  # the resident block rule (half the columns per block in the hierarchical gather's range)
+  # against the largest tile (GMAGG_RES_HALVE=0), over shapes incl. K <= 32 tiles
+  for r in 1 2; do
+    for h in 1 0; do
+      GMAGG_RES_HALVE=$h timeout -k 10 300 python -u tools/res_shape_bench.py \
+        --shapes 10x48670,20x48670,30x48670,32x60000,50x48670,64x60000,50x65000 --reps 5 \
+        | sed "s/}$/, \"halve\": $h}/" >> $O/h.jsonl || return 3
+    done
+  done
+  python3 - "$O" <<'PY'
+import collections, json, sys
+acc = collections.defaultdict(list)
+for l in open(sys.argv[1] + "/h.jsonl"):
+    r = json.loads(l)
+    acc[(r["K"], r["d"], r["halve"], r["exchange"], r["algo"])].append(r["us_per_iteration"])
+for k in sorted(acc):
+    print(k, " ".join(f"{v:.2f}" for v in acc[k]))
+PY
+}
+
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 O=gpurun_out/${2:-$1}
 mkdir -p "$O"
