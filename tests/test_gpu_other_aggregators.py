@@ -92,6 +92,33 @@ def test_coordinate_aggregators_special_values():
     assert rel_l2(t[ok].numpy(), tw[ok].numpy()) <= 1e-6
 
 
+@pytest.mark.parametrize("K", [129, 200, 256, 257, 512, 513, 1000, 1024])
+def test_staged_selection_special_values(K):
+    """The staged-transpose kernels (median K <= 1024, trimmed mean K <= 512) and the
+    branch-free slot keys at the tile boundaries: NaN columns (median NaN; trimmed mean per
+    torch's topk order), -0 / +0, infinities, all-negative columns, a ragged last tile."""
+    import byzantine_aircomp_amd as bz
+    d = 37
+    g = torch.Generator().manual_seed(K)
+    X = torch.randn(K, d, generator=g)
+    X[K // 2, 0] = float("nan")
+    X[: K // 3, 1] = float("nan")                      # NaNs reach the trimmed middle
+    X[:, 2] = 0.0
+    X[::2, 2] = -0.0
+    X[0, 3], X[1, 3] = float("inf"), float("-inf")
+    X[:, 4] = -X[:, 4].abs()
+    X[:, 5] = torch.round(X[:, 5])                      # ties
+    Xc = X.cuda()
+    m, want = bz.median(Xc).cpu(), orc.median(X)
+    assert torch.equal(torch.isnan(m), torch.isnan(want))
+    ok = ~torch.isnan(want)
+    assert torch.equal(m[ok], want[ok])
+    t, tw = bz.trimmed_mean(Xc).cpu(), orc.trimmed_mean(X)
+    assert torch.equal(torch.isnan(t), torch.isnan(tw))
+    ok = ~torch.isnan(tw)
+    assert rel_l2(t[ok].numpy(), tw[ok].numpy()) <= 1e-6
+
+
 @pytest.mark.parametrize("K,d,honest", [(129, 1001, 100), (300, 4096, 240), (260, 77, 200)])
 def test_krum_multi_tile_vs_oracle(K, d, honest):
     """Pair tiles of 128 rows: K spanning 2-3 row tiles, ragged d (scalar column tail)."""
