@@ -397,7 +397,7 @@ PY
 }
 
 st_tm() {
-  # the trimmed mean on the staged kernel (GMAGG_SELECT_ST=2) against col_select1 (default)
+  # the trimmed mean on the staged kernel (GMAGG_SELECT_ST=2) against the default
   for r in 1 2 3; do
     for v in 1 2; do
       GMAGG_SELECT_ST=$v timeout -k 10 200 python -u tools/select_bench.py --K 1000 400 256 --reps 5 \
