@@ -1455,7 +1455,10 @@ __global__ void __launch_bounds__(256) krum_cand_dist(const float* __restrict__ 
   typedef float f4 __attribute__((ext_vector_type(4)));
   typedef float f2 __attribute__((ext_vector_type(2)));
   __shared__ __attribute__((aligned(16))) float sC[kRefC / 2][kPC * 2];   // [pair][col][2]
-  __shared__ float sR[64][kPC + 1];
+  // rows as column PAIRS: sR2[c / 2][row] = (x[row][c], x[row][c + 1]), one ds_read_b64 per
+  // two columns (consecutive lanes, consecutive 8 B); row stride 65 pairs spreads the
+  // staging writes over the banks
+  __shared__ __attribute__((aligned(16))) float sR2[kPC / 2][65][2];
   const int tid = threadIdx.x, jl = tid & 63, grp = tid >> 6;
   const int64_t j = (int64_t)blockIdx.x * 64 + jl;
   const int64_t cb = (int64_t)blockIdx.y * chunk, ce = cb + chunk < d ? cb + chunk : d;
@@ -1497,8 +1500,8 @@ __global__ void __launch_bounds__(256) krum_cand_dist(const float* __restrict__ 
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int idx = tid + 256 * q, r = idx >> 3, cg = (idx & 7) * 4;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) sR[r][cg + u] = pr[q][u];
+      *reinterpret_cast<f2*>(&sR2[cg / 2][r][0]) = f2{pr[q][0], pr[q][1]};
+      *reinterpret_cast<f2*>(&sR2[cg / 2 + 1][r][0]) = f2{pr[q][2], pr[q][3]};
     }
     if (tid < 64 * NPP) {
 #pragma unroll
@@ -1511,7 +1514,8 @@ __global__ void __launch_bounds__(256) krum_cand_dist(const float* __restrict__ 
     for (int u = 0; u < NPP; ++u) acc[u] = f2{0.f, 0.f};
 #pragma unroll 4
     for (int c = 0; c < kPC; c += 2) {
-      const float x0 = sR[jl][c], x1 = sR[jl][c + 1];
+      const f2 xx = *reinterpret_cast<const f2*>(&sR2[c / 2][jl][0]);
+      const float x0 = xx[0], x1 = xx[1];
 #pragma unroll
       for (int u = 0; u < NPP; ++u) {
         const f4 cc = *reinterpret_cast<const f4*>(&sC[grp + 4 * u][2 * c]);

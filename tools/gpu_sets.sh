@@ -500,6 +500,30 @@ for k in sorted(acc):
 PY
 }
 
+krum_ab() {
+  # the Gram Krum path of this build against the previous build (libgmagg_old.so, copied
+  # aside): its tests, then krum_bench interleaved
+  timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+    tests/test_gpu_krum_gram.py > $O/t.log 2>&1 || { tail -30 $O/t.log; return 1; }
+  tail -1 $O/t.log
+  for r in 1 2 3; do
+    for v in "new:" "old:GMAGG_LIB=byzantine_aircomp_amd/libgmagg_old.so"; do
+      n=${v%%:*}; e=${v#*:}
+      env $e timeout -k 10 300 python -u tools/krum_bench.py --shapes 256x4194304,256x1048576,64x1048576 \
+        --reps 5 | grep '"gram"' | sed "s/}$/, \"v\": \"$n\"}/" >> $O/k.jsonl || return 2
+    done
+  done
+  python3 - "$O" <<'PY'
+import collections, json, sys
+acc = collections.defaultdict(list)
+for l in open(sys.argv[1] + "/k.jsonl"):
+    r = json.loads(l)
+    acc[(r["K"], r["d"], r["v"])].append(r["ms"])
+for k in sorted(acc):
+    print(k, " ".join(f"{v:.3f}" for v in acc[k]))
+PY
+}
+
 [ $# -ge 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 SET [TAG]  (sets: $(declare -F | awk '{print $3}' | tr '\n' ' '))"; exit 2; }
 O=gpurun_out/${2:-$1}
 mkdir -p "$O"
