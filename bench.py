@@ -712,14 +712,18 @@ def launch_ranks(n: int, argv, cmd=None, poll_s: float = 0.2) -> int:
     This process makes no GPU call: it only spawns and waits.  `cmd` replaces the worker
     command line (tests)."""
     import subprocess
+    import tempfile
     cmd = cmd or [sys.executable, os.path.abspath(__file__), *argv]
     port = free_port()
     procs = []
+    # rank 0's stdout goes to a file, read once every rank has exited (a pipe read only at
+    # the end would block a rank that writes more than the pipe holds; ADVICE r5)
+    out0 = tempfile.TemporaryFile()
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
-        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else
+        procs.append(subprocess.Popen(cmd, env=env, stdout=out0 if r == 0 else
                                       subprocess.DEVNULL))
     rc = 0
     live = set(range(n))
@@ -739,7 +743,9 @@ def launch_ranks(n: int, argv, cmd=None, poll_s: float = 0.2) -> int:
             time.sleep(poll_s)
     for p in procs:
         p.wait()
-    out = procs[0].stdout.read().decode(errors="replace") if procs[0].stdout else ""
+    out0.seek(0)
+    out = out0.read().decode(errors="replace")
+    out0.close()
     lines = [ln for ln in out.splitlines() if ln.strip()]
     if lines:
         sys.stdout.write(lines[-1] + "\n")
@@ -750,13 +756,41 @@ def launch_ranks(n: int, argv, cmd=None, poll_s: float = 0.2) -> int:
     return rc
 
 
+def visible_gpus():
+    """GPUs this process could open, counted WITHOUT any GPU-library call (the launcher
+    parent must not initialise a GPU runtime before it spawns the ranks): the KFD topology's
+    GPU nodes (gpu_id != 0), narrowed by HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES when set.  None when the topology cannot be read."""
+    import glob
+    n = 0
+    try:
+        for node in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id"):
+            with open(node) as f:
+                n += int(f.read().strip() or "0") != 0
+    except (OSError, ValueError):
+        return None
+    if n == 0:
+        return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def main():
     args = parse()
+    if args.workload == "c5" and args.problems // len(C5_VARS) < args.gpus:
+        # every rank takes a contiguous share of each var group: no empty ranks (ADVICE r5)
+        raise SystemExit(f"c5: --problems {args.problems} gives {args.problems // len(C5_VARS)} "
+                         f"problems per var group, fewer than --gpus {args.gpus}")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        # the driver's plain `python bench.py --gpus N`: become the launcher (before any GPU
-        # call; counting devices does not initialise the GPU on this image)
-        if not args.one_gpu and torch.cuda.device_count() < args.gpus:
-            raise SystemExit(f"--gpus {args.gpus} but {torch.cuda.device_count()} GPU(s) visible")
+        # the driver's plain `python bench.py --gpus N`: become the launcher.  No GPU-library
+        # call here (not even a device count): the GPUs are counted from the KFD topology, and
+        # where that is unreadable the ranks find out themselves and fail loudly
+        n_vis = None if args.one_gpu else visible_gpus()
+        if n_vis is not None and n_vis < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but {n_vis} GPU(s) visible")
         raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
     if os.environ.get("BENCH_EXIT_MAPS"):
         # diagnostics: this process's memory map as the interpreter exits, to attribute

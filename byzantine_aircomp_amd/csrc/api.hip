@@ -458,9 +458,11 @@ int run_resident(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ldx,
   r.last_movement = hst->last_movement;
   r.converged = hst->converged;
   r.algo_used = GM_ALGO_RESIDENT;
-  // bar[0] = 1 + local (group 0's, for the hierarchical gather)
-  r.exchange = hbar[0] != 2 ? GM_EXCHANGE_AGENT
-               : a.hier ? GM_EXCHANGE_XCD_HIER
+  // The hierarchical gather ran whenever a.hier is set (its member granules are L2-kept
+  // only where the check-in confirmed a group on one XCD; ADVICE r5: report the gather that
+  // ran, as run_resident_batched does).  Otherwise bar[0] = 1 + local.
+  r.exchange = a.hier ? GM_EXCHANGE_XCD_HIER
+               : hbar[0] != 2 ? GM_EXCHANGE_AGENT
                : a.split ? GM_EXCHANGE_XCD_SPLIT : GM_EXCHANGE_XCD_LOCAL;
   if (res) *res = r;
   return GM_OK;
@@ -1602,15 +1604,15 @@ int gm_krum_panels_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t 
 }
 
 // Krum through the Gram MFMA kernel (coordinate.hip krum_gram_bounds: the bounds, the
-// candidates, the exact recomputation).  epsg bounds |G~_ij - G_ij| / (n_i n_j) for the
-// scaled-f16 split (gram.hip): the split's dropped terms (<= 3 * 2^-22), the fp32 chain of
-// one flush period (kH16Flush stages x 64 columns = 8192 columns, 3 products: <= 768
-// accumulator roundings + the 32-term MFMA sums + the fp32 partial, <= 800 * 2^-24), the
-// centring rounding (2^-24 each side) and the f16 subnormal floor (2^-27 of the row's
-// largest element per element: <= 2^-27 sqrt(d) by Cauchy-Schwarz), rounded up to 6e-5.
-static double krum_gram_eps(int64_t d) {
-  return 6e-5 + std::ldexp(1.0, -27) * std::sqrt((double)d);
-}
+// candidates, the exact recomputation).  epsg bounds the relative error |G~_ij - G_ij| /
+// (n_i n_j) of the scaled-f16 split (gram.hip): the split's dropped terms (<= 3 * 2^-22),
+// the fp32 chain of one flush period (kH16Flush stages x 64 columns = 8192 columns, 3
+// products: <= 768 accumulator roundings + the 32-term MFMA sums + the fp32 partial,
+// <= 800 * 2^-24) and the centring rounding (2^-24 each side), rounded up to 6e-5.  The f16
+// subnormal floor is an ABSOLUTE error set by each column block's shared scale (one large
+// row raises it for every row of the block): krum_gram_bounds adds it from the exponents
+// the Gram kernel exports (a per-row bound was assumed here before).
+static double krum_gram_eps() { return 6e-5; }
 
 // GMAGG_KRUM: 0 exact pair distances only, 1 the Gram path wherever it is eligible, 2
 // (default) AUTO: the Gram path at K >= 64 and K^2 d >= 2^29 (it measured faster on every
@@ -1659,7 +1661,9 @@ static int krum_gram(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
     HIPCHK(launch_gram(X, K, d, ws ? W : ldx, p, GramKind::H16, gg, w.gslab, w.G, w.st, s,
                        ws ? ldx : 0, ws));
     HIPCHK(launch_gram_check(w.G, KP, w.st, s));
-    HIPCHK(launch_krum_gram_select(w.G, KP, K, kk, krum_gram_eps(d), w.alpha, w.u, maxc, cand, s));
+    HIPCHK(launch_krum_gram_select(w.G, KP, K, kk, krum_gram_eps(),
+                                   gram_block_exp(w.gslab, KT, gg), gg.nb, d, w.alpha, w.u, maxc,
+                                   cand, s));
     HIPCHK(hipMemcpyAsync(hst, w.st, sizeof(KState), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(hcand, cand, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(hcand + 1, cand + maxc + 1, sizeof(int64_t), hipMemcpyDeviceToHost, s));

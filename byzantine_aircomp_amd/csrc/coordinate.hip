@@ -1353,10 +1353,17 @@ __global__ void __launch_bounds__(256) copy_row(const float* __restrict__ X, int
 // ---------------------------------------------------------------------------
 // Krum through the Gram MFMA kernel (round 5; SURVEY §8 f3: D = diag(G) 1^T + 1 diag(G)^T
 // - 2G).  G~ = (X - p)(X - p)^T from gram.hip's scaled-f16 split (p = row 0), then
-//   D~_ij = G~_ii + G~_jj - 2 G~_ij,  |D_ij - D~_ij| <= e_ij = epsg (n_i + n_j)^2 + 1e-5 |D~_ij|
-// (n_i = ||x_i - p||; epsg bounds |G~ - G| / (n_i n_j): the split's 2^-22 terms, the fp32
-// accumulation chains between flushes, the f16 subnormal floor — api.hip krum_gram_eps; the
-// 1e-5 |D~| covers the exact path's own fp32 rounding).  A row's score is the sum of its kk
+//   D~_ij = G~_ii + G~_jj - 2 G~_ij,
+//   |D_ij - D~_ij| <= e_ij = epsg (n_i + n_j)^2 + 4 A (n_i + n_j) + 4 A^2 + 1e-5 |D~_ij|
+// (n_i = ||x_i - p||.  epsg bounds the RELATIVE errors |G~ - G| / (n_i n_j): the split's
+// 2^-22 terms, the fp32 accumulation chains between flushes, the centring — api.hip
+// krum_gram_eps.  A bounds the ABSOLUTE part, the f16 subnormal floor: the Gram kernel
+// scales every element of a column block by ONE power of two 2^e_b, chosen from the block's
+// largest |x - p| over all rows (gram.hip h16_producer), so an element's split loses up to
+// 2^-25 2^-e_b whatever its own row's size — one large (Byzantine) row raises it for every
+// honest row of the block.  With E = max_b 2^-e_b, ||delta_i|| <= A = 2^-25 E sqrt(d), and
+// |G~_ij - G_ij| <= A (n_i + n_j) + A^2, so D~ is off by <= 4 A (n_i + n_j) + 4 A^2.  The
+// 1e-5 |D~| covers the exact path's own fp32 rounding.)  A row's score is the sum of its kk
 // smallest distances (self = 0), monotone in each distance, so
 //   LB_i = score(max(0, D~ - e)) <= score_i <= UB_i = score(D~ + e).
 // Every row with LB_i <= min_j UB_j is a candidate — the exact argmin always is — and the
@@ -1368,20 +1375,34 @@ __global__ void __launch_bounds__(256) copy_row(const float* __restrict__ X, int
 // gives NaN, which sends the call to the exact path.
 __global__ void __launch_bounds__(256) krum_gram_bounds(const double* __restrict__ G, int KP,
                                                         int64_t K, int64_t kk, double epsg,
-                                                        double* __restrict__ lb,
+                                                        const int* __restrict__ bexp, int nb,
+                                                        int64_t d, double* __restrict__ lb,
                                                         double* __restrict__ ub) {
   extern __shared__ double sb[];
   double* sl = sb;
   double* su = sb + K;
   __shared__ double scratch[8];
+  __shared__ int s_emin;
   const int64_t i = blockIdx.x;
+  // A = 2^-25 max_b 2^-e_b sqrt(d): the smallest block exponent (the largest block scale)
+  int em = 1 << 20;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) em = min(em, bexp[b]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) em = min(em, __shfl_xor(em, o, 64));
+  if (threadIdx.x == 0) s_emin = 1 << 20;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) atomicMin(&s_emin, em);
+  __syncthreads();
+  const double A = s_emin >= (1 << 20) ? 0.0 : ldexp(sqrt((double)d), -25 - s_emin);
+  // n_i from G~_ii: G~_ii >= (1 - 2 epsg) n_i^2 - 2 A n_i - A^2, so n_i <= this + 3 A
   const double gii = G[i * KP + i];
-  const double ni = sqrt(fmax(gii, 0.0) * (1.0 + 2.0 * epsg));
+  const double ni = sqrt(fmax(gii, 0.0) * (1.0 + 2.0 * epsg)) + 3.0 * A;
   for (int64_t j = threadIdx.x; j < K; j += blockDim.x) {
     const double gjj = G[j * KP + j];
-    const double nj = sqrt(fmax(gjj, 0.0) * (1.0 + 2.0 * epsg));
+    const double nj = sqrt(fmax(gjj, 0.0) * (1.0 + 2.0 * epsg)) + 3.0 * A;
     const double dt = (gii + gjj) - 2.0 * G[i * KP + j];
-    const double e = epsg * (ni + nj) * (ni + nj) + 1e-5 * fabs(dt);
+    const double e = epsg * (ni + nj) * (ni + nj) + 4.0 * A * (ni + nj) + 4.0 * A * A +
+                     1e-5 * fabs(dt);
     const double hi = dt + e;
     sl[j] = j == i ? 0.0 : fmax(dt - e, 0.0);
     su[j] = j == i ? 0.0 : (hi >= 0.0 ? hi : __builtin_nan(""));
@@ -1771,10 +1792,10 @@ hipError_t launch_copy_row_k(const float* X, int64_t d, int64_t ldx, int ws, int
 }
 
 hipError_t launch_krum_gram_select(const double* G, int KP, int64_t K, int64_t kk, double epsg,
-                                   double* lb, double* ub, int64_t maxc, int64_t* cand,
-                                   hipStream_t s) {
+                                   const int* bexp, int nb, int64_t d, double* lb, double* ub,
+                                   int64_t maxc, int64_t* cand, hipStream_t s) {
   hipLaunchKernelGGL(krum_gram_bounds, dim3((unsigned)K), dim3(256), 2 * sizeof(double) * K, s, G,
-                     KP, K, kk, epsg, lb, ub);
+                     KP, K, kk, epsg, bexp, nb, d, lb, ub);
   hipLaunchKernelGGL(krum_candidates, dim3(1), dim3(64), 0, s, lb, ub, K, maxc, cand);
   return hipGetLastError();
 }

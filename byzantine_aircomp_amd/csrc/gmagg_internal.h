@@ -222,6 +222,8 @@ struct GramGrid {
 int gram_kt(int64_t K);
 GramGrid gram_grid(int64_t d, GramKind kind, int num_cu);
 size_t gram_slab_floats(int KT, const GramGrid& g);
+// the f16 kernel's per-block scale exponents (written by every H16 launch_gram)
+int* gram_block_exp(float* slab, int KT, const GramGrid& g);
 // pstride > 0: X in the panel layout [ceil(d/W)][K][W], W = 1 << wshift (H16 only).
 hipError_t launch_gram(const float* X, int64_t K, int64_t d, int64_t ldx, const float* p,
                        GramKind kind, const GramGrid& g, float* slab, double* G, KState* st,
@@ -256,8 +258,8 @@ hipError_t launch_krum(const float* X, int64_t K, int64_t d, int64_t ldx, int64_
 hipError_t launch_copy_row_k(const float* X, int64_t d, int64_t ldx, int ws, int64_t k, float* out,
                              hipStream_t s);
 hipError_t launch_krum_gram_select(const double* G, int KP, int64_t K, int64_t kk, double epsg,
-                                   double* lb, double* ub, int64_t maxc, int64_t* cand,
-                                   hipStream_t s);
+                                   const int* bexp, int nb, int64_t d, double* lb, double* ub,
+                                   int64_t maxc, int64_t* cand, hipStream_t s);
 int krum_refine_max();
 hipError_t launch_krum_refine(const float* X, int64_t K, int64_t d, int64_t ldx, int ws,
                               const int64_t* cidx, int m, int64_t kk, double* part, double* Dc,

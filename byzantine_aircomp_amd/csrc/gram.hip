@@ -734,7 +734,8 @@ __device__ __forceinline__ void h16_producer(const float* __restrict__ X, int64_
                                              int64_t pstride,
                                              const float* __restrict__ p, int64_t c_begin,
                                              int64_t c_end, int nstage, H16Lds<KT>& lds,
-                                             int* s_exp, float* s_bmax) {
+                                             int* s_exp, float* s_bmax,
+                                             int* __restrict__ bexp) {
   constexpr int RPT = GramShape<KT>::ROWS_PER_THREAD;
   using Str = H16Stream<KT, kH16Sets, WS>;
   Str P;
@@ -746,6 +747,7 @@ __device__ __forceinline__ void h16_producer(const float* __restrict__ X, int64_
   if (nstage == 0 || DBG == 2) {                 // no columns: meet the consumers' barriers
     if (DBG == 2)
       for (int k = t; k < GramShape<KT>::KP; k += 256) s_exp[k] = 0;
+    if (t == 0) bexp[blockIdx.x] = DBG == 2 ? 0 : 100;   // (no elements: no rounding)
     for (int s = 0; s <= (DBG == 2 ? nstage : 0) + 1; ++s) __syncthreads();   // DBG 2: no loads
     return;
   }
@@ -775,6 +777,10 @@ __device__ __forceinline__ void h16_producer(const float* __restrict__ X, int64_
     e = e < -100 ? -100 : (e > 100 ? 100 : e);
     P.sb = ldexpf(1.f, e);
     for (int k = t; k < GramShape<KT>::KP; k += 256) s_exp[k] = e;
+    // the block's exponent for the callers that bound the split's absolute error (Krum:
+    // an element's f16 subnormal floor is 2^-25 of the SCALED value, 2^-25 2^-e unscaled,
+    // whatever row it belongs to; coordinate.hip krum_gram_bounds)
+    if (t == 0) bexp[blockIdx.x] = e;
   }
   P.template commit_refetch<0>(lds[0][0], lds[0][1], min(2, last));
   __syncthreads();                               // stage 0 in buffer 0, exponents published
@@ -905,7 +911,8 @@ __global__ void __launch_bounds__(512, 1) gram_h16_partial(const float* __restri
                                                            int64_t d, int64_t ldx, int64_t pstride,
                                                            const float* __restrict__ p,
                                                            int64_t cols_per_block, int nseg,
-                                                           float* __restrict__ slab) {
+                                                           float* __restrict__ slab,
+                                                           int* __restrict__ bexp) {
   __shared__ H16Lds<KT> lds;
   __shared__ int s_exp[GramShape<KT>::KP];
   __shared__ float s_bmax[4];
@@ -914,7 +921,8 @@ __global__ void __launch_bounds__(512, 1) gram_h16_partial(const float* __restri
   const int64_t c_end = c_begin + cols_per_block < d ? c_begin + cols_per_block : d;
   const int nstage = c_begin < c_end ? (int)((c_end - c_begin + kH16BK - 1) / kH16BK) : 0;
   if (w >= 4) {
-    h16_producer<KT, DBG, WS>(X, K, ldx, pstride, p, c_begin, c_end, nstage, lds, s_exp, s_bmax);
+    h16_producer<KT, DBG, WS>(X, K, ldx, pstride, p, c_begin, c_end, nstage, lds, s_exp, s_bmax,
+                              bexp);
     return;
   }
 #if GMK_H16_SHAPE == 16
@@ -1137,9 +1145,16 @@ static hipError_t launch_gram_kt(const float* X, int64_t K, int64_t d, int64_t l
 
 int gram_kt(int64_t K) { return K <= 32 ? 1 : K <= 64 ? 2 : K <= 128 ? 4 : K <= 256 ? 8 : 0; }
 
-// partials [nb * nseg][tiles][1024] fp32, then the reduction's fp64 tmp[kReduceGroups][n]
+// partials [nb * nseg][tiles][1024] fp32, then the reduction's fp64 tmp[kReduceGroups][n],
+// then the f16 kernel's per-block scale exponents [nb] (int)
 size_t gram_slab_floats(int KT, const GramGrid& g) {
-  return (size_t)(g.nb * g.nseg + 2 * kReduceGroups) * (KT * (KT + 1) / 2) * 1024;
+  return (size_t)(g.nb * g.nseg + 2 * kReduceGroups) * (KT * (KT + 1) / 2) * 1024 +
+         (size_t)(g.nb + 1) / 2 * 2;
+}
+
+int* gram_block_exp(float* slab, int KT, const GramGrid& g) {
+  return reinterpret_cast<int*>(slab + (size_t)(g.nb * g.nseg + 2 * kReduceGroups) *
+                                           (KT * (KT + 1) / 2) * 1024);
 }
 
 template <int KT>
@@ -1163,11 +1178,11 @@ static hipError_t launch_split_kt(const float* X, int64_t K, int64_t d, int64_t 
 template <int KT, int DBG>
 static hipError_t launch_h16_dbg(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t pstride,
                                  int wshift, const float* p, int nb, int64_t cpb, int nseg,
-                                 float* slab, hipStream_t s) {
+                                 float* slab, int* bexp, hipStream_t s) {
   // panel widths of the Gram tiles (gm_panel_width at K <= 256): 64, 128, 256
 #define GMK_H16_LAUNCH(WS_)                                                                  \
   hipLaunchKernelGGL((gram_h16_partial<KT, DBG, WS_>), dim3(nb), dim3(512), 0, s, X, K, d, ldx, \
-                     pstride, p, cpb, nseg, slab)
+                     pstride, p, cpb, nseg, slab, bexp)
   if (!pstride) GMK_H16_LAUNCH(0);
   else if (wshift == 7) GMK_H16_LAUNCH(7);
   else if (wshift == 6) GMK_H16_LAUNCH(6);
@@ -1180,16 +1195,16 @@ static hipError_t launch_h16_dbg(const float* X, int64_t K, int64_t d, int64_t l
 template <int KT>
 static hipError_t launch_h16_kt(const float* X, int64_t K, int64_t d, int64_t ldx, int64_t pstride,
                                 int wshift, const float* p, int nb, int64_t cpb, int nseg,
-                                float* slab, hipStream_t s) {
+                                float* slab, int* bexp, hipStream_t s) {
   // GMAGG_GRAM_DEBUG = 1 / 2: timing probes without MFMAs / without loads (wrong G)
   static const int dbg = [] { const char* e = getenv("GMAGG_GRAM_DEBUG"); return e ? atoi(e) : 0; }();
   hipError_t e;
   if (KT == 8 && dbg == 1)   // probes built for the 256-row tile only
-    e = launch_h16_dbg<KT, KT == 8 ? 1 : 0>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, s);
+    e = launch_h16_dbg<KT, KT == 8 ? 1 : 0>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, bexp, s);
   else if (KT == 8 && dbg == 2)
-    e = launch_h16_dbg<KT, KT == 8 ? 2 : 0>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, s);
+    e = launch_h16_dbg<KT, KT == 8 ? 2 : 0>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, bexp, s);
   else
-    e = launch_h16_dbg<KT, 0>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, s);
+    e = launch_h16_dbg<KT, 0>(X, K, d, ldx, pstride, wshift, p, nb, cpb, nseg, slab, bexp, s);
   return e != hipSuccess ? e : hipGetLastError();
 }
 
@@ -1227,11 +1242,12 @@ hipError_t launch_gram(const float* X, int64_t K, int64_t d, int64_t ldx, const 
   const int64_t cpb = g.cpb;
   hipError_t e;
   if (kind == GramKind::H16) {
+    int* bexp = gram_block_exp(slab, KT, g);
     switch (KT) {
-      case 1: e = launch_h16_kt<1>(X, K, d, ldx, pstride, wshift, p, nb, cpb, g.nseg, slab, s); break;
-      case 2: e = launch_h16_kt<2>(X, K, d, ldx, pstride, wshift, p, nb, cpb, g.nseg, slab, s); break;
-      case 4: e = launch_h16_kt<4>(X, K, d, ldx, pstride, wshift, p, nb, cpb, g.nseg, slab, s); break;
-      case 8: e = launch_h16_kt<8>(X, K, d, ldx, pstride, wshift, p, nb, cpb, g.nseg, slab, s); break;
+      case 1: e = launch_h16_kt<1>(X, K, d, ldx, pstride, wshift, p, nb, cpb, g.nseg, slab, bexp, s); break;
+      case 2: e = launch_h16_kt<2>(X, K, d, ldx, pstride, wshift, p, nb, cpb, g.nseg, slab, bexp, s); break;
+      case 4: e = launch_h16_kt<4>(X, K, d, ldx, pstride, wshift, p, nb, cpb, g.nseg, slab, bexp, s); break;
+      case 8: e = launch_h16_kt<8>(X, K, d, ldx, pstride, wshift, p, nb, cpb, g.nseg, slab, bexp, s); break;
       default: return hipErrorInvalidValue;
     }
   } else {

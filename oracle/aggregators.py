@@ -206,7 +206,8 @@ class CountWindow:
 
 
 def gm2_count_window(X: torch.Tensor, guess: Optional[torch.Tensor] = None, maxiter: int = 200,
-                     tol: float = 1e-5, floor_ulps: float = FLOOR_ULPS) -> CountWindow:
+                     tol: float = 1e-5, floor_ulps: float = FLOOR_ULPS,
+                     chunk_rows: Optional[int] = None) -> CountWindow:
     """Is "the same iteration count +-1" (north_star) well posed on this input?
 
     The reference stops at the first t with ||g_t - g_{t+1}|| <= tol (M:180-183), on
@@ -222,16 +223,26 @@ def gm2_count_window(X: torch.Tensor, guess: Optional[torch.Tensor] = None, maxi
     see a movement below tol (it stops only if rounding happens to land it there, or on
     an exact fixed point of its own arithmetic), so no count is certain and a test must
     state its own bar.  Runs the exact (fp64) iteration until the movement is below
-    tol - delta."""
-    X64 = X.double()
-    g = (X64.mean(dim=0) if guess is None else guess.double())
+    tol - delta.  ``chunk_rows``: convert and process X that many rows at a time (bounded
+    fp64 temporaries for large inputs; the same iteration up to fp64 summation order)."""
+    K = X.shape[0]
+    step = K if chunk_rows is None else max(1, int(chunk_rows))
+    X64 = X.double() if step >= K else None
+
+    def rows(k0):
+        return X64[k0:k0 + step] if X64 is not None else X[k0:k0 + step].double()
+
+    g = (sum(rows(k0).sum(dim=0) for k0 in range(0, K, step)) / K if guess is None
+         else guess.double())
     early = late = None
     undetermined = False
     max_norm = float(torch.linalg.vector_norm(g))
     for t in range(1, maxiter + 1):
-        dist = torch.clamp(torch.linalg.vector_norm(X64 - g, dim=1), min=CLAMP)
+        dist = torch.cat([torch.linalg.vector_norm(rows(k0) - g, dim=1)
+                          for k0 in range(0, K, step)])
+        dist = torch.clamp(dist, min=CLAMP)
         w = 1.0 / dist
-        nxt = (w @ X64) / w.sum()
+        nxt = sum(w[k0:k0 + step] @ rows(k0) for k0 in range(0, K, step)) / w.sum()
         moved = float(torch.linalg.vector_norm(g - nxt))
         max_norm = max(max_norm, float(torch.linalg.vector_norm(nxt)))
         delta = floor_ulps * 2.0 ** -24 * max_norm

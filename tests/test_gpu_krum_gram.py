@@ -154,3 +154,23 @@ def test_gram_krum_panels_ragged(monkeypatch):
     b = bz.Krum(X, {"honestSize": 160})
     assert info["algo"] == "gram" or info["reason"] == "candidates", info
     assert bz.aggregators.Krum.last_index == ia and torch.equal(a, b)
+
+
+@pytest.mark.parametrize("scale", [1e3, 1e6])
+def test_gram_krum_huge_byzantine_rows(scale, monkeypatch):
+    """Byzantine rows `scale` x the honest spread: the Gram kernel's f16 scale is
+    one power of two per column block, set by the block's largest |x - p| — a Byzantine row —
+    so the honest rows' elements sit scale-times lower in f16 (near or in the subnormal
+    range at 1e6).  The bounds carry that absolute error (krum_gram_bounds' A term, from the
+    exported block exponents): the Gram path either returns the exact path's row or, when
+    the bounds leave too many candidates, hands the call to the exact path."""
+    g = torch.Generator().manual_seed(int(scale) % 1000 + 5)
+    K, d, honest = 128, 65_536, 103
+    X = 0.05 * torch.randn(K, d, generator=g)
+    X[honest:] = scale * (0.25 + 0.5 * torch.randn(K - honest, d, generator=g))
+    X = X[torch.randperm(K, generator=g)].contiguous()
+    if bool(torch.all(X[0].abs() > 1.0)):            # keep an honest centre row
+        X[[0, 1]] = X[[1, 0]]
+    a, ia, info, b, ib = _both(X.cuda(), honest, monkeypatch)
+    assert info["algo"] == "gram" or info["reason"] in ("candidates", "gram_nonfinite"), info
+    assert ia == ib and torch.equal(a, b), (ia, ib, info)

@@ -12,6 +12,7 @@
 #   trace:NAME[:ARGS]         rocprofv3 --kernel-trace --stats of bench.py ARGS -> NAME/
 #   pmc:NAME:COUNTER[:ARGS]   one rocprofv3 --pmc pass (one counter) of bench.py ARGS
 #   py:NAME:SCRIPT[:ARGS]     python SCRIPT ARGS -> NAME.log (tools/*.py probes)
+#   run:NAME:CMD              a built probe binary (tools/*.hip) -> NAME.log
 #   env:VAR=VALUE             export for the following steps
 set -o pipefail
 tag=$1
@@ -61,6 +62,11 @@ for step in "$@"; do
       name=${rest%%:*}; r2=${rest#*:}; script=${r2%%:*}; args=${r2#*:}; [ "$args" = "$r2" ] && args=""
       timeout -k 10 900 python -u "$script" $args > "$out/$name.log" 2>&1 \
         || { rc=$?; tail -30 "$out/$name.log"; exit $rc; }
+      tail -40 "$out/$name.log"
+      ;;
+    run)
+      name=${rest%%:*}; cmd=${rest#*:}
+      timeout -k 10 600 $cmd > "$out/$name.log" 2>&1 || { rc=$?; tail -30 "$out/$name.log"; exit $rc; }
       tail -40 "$out/$name.log"
       ;;
     *)
