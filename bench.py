@@ -150,7 +150,9 @@ def pmc_traffic(workload, layout, kernel="weiszfeld_pass", mode="0"):
         files = [f for f in files if "aircomp" not in os.path.basename(f)]
     for path in sorted(files, key=profile_order, reverse=True):
         data = json.load(open(path))
-        for name, row in data["kernels"].items():
+        for name, row in data.get("kernels", {}).items():
+            if "hbm_bytes_per_launch" not in row:      # (a pass without the traffic summary)
+                continue
             if kernel == "weiszfeld_pass":
                 m = re.search(r"weiszfeld_pass<([^>]*)>", name)
                 if not m:

@@ -1205,9 +1205,11 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
     }
     ka.do_check = 1;
     ka.do_coef = last ? 0 : 1;
+    // lagged poll: the K-space step itself leaves its KState in the host-mapped slot
+    ka.mirror = lagged && !last ? &hslot[t & 1] : nullptr;
     HIPCHK(launch_kspace(ka, s));
+    ka.mirror = nullptr;
     if (lagged && !last) {
-      HIPCHK(hipMemcpyAsync(&hslot[t & 1], w.st, sizeof(KState), hipMemcpyDeviceToHost, s));
       HIPCHK(hipEventRecord(c->poll_ev[t & 1], s));
       if (pending >= 0) {
         HIPCHK(hipEventSynchronize(c->poll_ev[pending & 1]));

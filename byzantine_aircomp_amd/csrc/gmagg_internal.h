@@ -87,6 +87,7 @@ struct KspaceArgs {
   // Batched: blockIdx.x = problem; sums advance by sums_ps, r / coef by K, st by 1.
   int64_t sums_ps;
   int* n_done;            // problems whose tol test has fired (nullable)
+  KState* mirror;         // host-mapped copy of *st written at the end (nullable, one problem)
 };
 
 // Streaming pass (stream_pass.hip).  mode: 0 step, 1 init, 2 init + ||x_k||^2, 3 Gram

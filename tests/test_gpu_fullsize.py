@@ -105,7 +105,7 @@ def test_c3_full_size_panels_fixed_point():
 
 
 def test_c4_shard_full_size_gram_fixed_point():
-    """One GPU's C4 shard exactly: 256 x 15.625M, AUTO -> guarded split-bf16 Gram."""
+    """One GPU's C4 shard exactly: 256 x 15.625M, AUTO -> the guarded scaled-f16 split Gram."""
     m = bz()
     K, d = 256, 15_625_000
     X, g0 = _fill(K, d, 51)

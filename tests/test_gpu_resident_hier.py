@@ -181,8 +181,6 @@ def test_batched_hier_vs_flat(agg, mode, monkeypatch):
     (a, ra), (b, rb) = outs[mode], outs["0"]
     assert (ra[0].exchange == "xcd_hier") == (mode == "1") and rb[0].exchange != "xcd_hier"
     assert [r.iters for r in ra] == [r.iters for r in rb]
-    if mode == "2":
-        assert torch.equal(a, b)
     assert rel_l2(a.numpy(), b.numpy()) <= (1e-6 if agg == "gm2" else 1e-5)
     q = 5
     if agg == "gm2":

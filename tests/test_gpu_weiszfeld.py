@@ -383,7 +383,8 @@ def _c4_like(K, d, seed=20211):
 
 
 def test_gram_split_vs_f32_and_auto_choice():
-    """The split-bf16 Gram agrees with the exact f32-MFMA Gram; AUTO keeps it (guard passes)."""
+    """The scaled-f16 split Gram (algo="gram") agrees with the exact f32-MFMA Gram; AUTO keeps it
+    (guard passes)."""
     m = bz()
     X, g0 = _c4_like(256, 1 << 20)
     a = m.gm2(X, {"maxiter": 1000, "guess": g0, "algo": "gram_f32"})
