@@ -95,6 +95,9 @@ struct KspaceArgs {
 hipError_t launch_pass(const PassCfg& cfg, int mode, int grid, const PassArgs& a, hipStream_t s,
                        int problems = 1);
 int pass_blocks_per_cu(const PassCfg& cfg, int mode);
+// The row-major gm2 STEP / INIT at 512 < K <= 1024 on 32 waves per CU (rows_pass.hip).
+bool rows_pass_eligible(const PassArgs& a, int mode);
+hipError_t launch_rows_pass(int mode, int grid, const PassArgs& a, hipStream_t s);
 bool pass_cfg_supported(const PassCfg& cfg);
 
 // Reduction, K-space step and the two-pass path (weiszfeld.hip).

@@ -455,6 +455,11 @@ bool pass_cfg_supported(const PassCfg& cfg) { return pass_kernel(cfg, 0) != null
 
 hipError_t launch_pass(const PassCfg& cfg, int mode, int grid, const PassArgs& a, hipStream_t s,
                        int problems) {
+  // the K <= 1024 row-major tile's gm2 passes: the 32-wave rows kernel (rows_pass.hip), the
+  // same two blocks per CU, so the same grid and slab
+  if (problems == 1 && cfg.V == 4 && cfg.NW == 8 && cfg.LPR == 8 && cfg.R == 16 && cfg.OCC == 2 &&
+      rows_pass_eligible(a, mode))
+    return launch_rows_pass(mode, grid, a, s);
   const void* fn = pass_kernel(cfg, mode, a.panel_stride > 0);
   if (!fn) return hipErrorInvalidValue;
   void* args[] = {const_cast<PassArgs*>(&a)};

@@ -4,7 +4,8 @@ Same values, same chunks, same reduction order as the row-major call with the
 float4 tile (d % 4 == 0), so the aggregate, the iteration count and the last
 movement must be BIT-identical to gm2 / gm on the [K, d] tensor — which the
 row-major tests pin to the reference (test_gpu_weiszfeld.py); other d within
-rounding; plus the reference's golden vectors directly.
+rounding, and so is row-major gm2 at 512 < K <= 1024, which runs the 32-wave rows
+kernel (rows_pass.hip, round 6); plus the reference's golden vectors directly.
 """
 import numpy as np
 import pytest
@@ -57,8 +58,13 @@ def test_panels_bit_identical_to_rows(K, d, agg):
     assert rb.algo == "stream"
     if d % 4 == 0 and not (32 < K <= 64 or 128 < K <= 256):
         # the row-major call runs the same float4 tile: same chunks, same order (at
-        # 32 < K <= 64 and 128 < K <= 256 panels have a tile of their own, api.hip pick_cfg)
-        assert torch.equal(a, b)
+        # 32 < K <= 64 and 128 < K <= 256 panels have a tile of their own, api.hip pick_cfg;
+        # row-major gm2 at 512 < K <= 1024 runs the 32-wave rows kernel, rows_pass.hip,
+        # whose column sums take another order: equal to rounding)
+        if agg == "gm2" and 512 < K <= 1024:
+            assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 1e-6
+        else:
+            assert torch.equal(a, b)
         assert (ra.iters, ra.converged) == (rb.iters, rb.converged)
         assert ra.last_movement == rb.last_movement or (np.isnan(ra.last_movement)
                                                         and np.isnan(rb.last_movement))

@@ -191,15 +191,17 @@ def test_sharded_gram_equals_unsharded(algo):
 @pytest.mark.parametrize("P", [2, 3])
 @pytest.mark.parametrize("check_every", [0, 1])
 def test_sharded_panels_equal_sharded_rows(P, check_every):
-    """Each rank's shard in the panel layout: the same chunks and reduction order
-    as the row-major shard (d_local % 4 == 0), so bit-identical results."""
+    """Each rank's shard in the panel layout against the row-major shard (d_local % 4 == 0):
+    the same chunks per block, the same iteration count; at K = 1000 the row-major gm2
+    passes run the 32-wave rows kernel (rows_pass.hip), which sums a column's rows in
+    another order, so the results agree to rounding (bit for bit before round 6)."""
     X, p = _problem(1000, 40_960, 200, seed=20 + P)
     opts = {"maxiter": 1000, "tol": 1e-5}
     rows, it_r = _sharded(X, p, P, opts, aircomp=False, check_every=check_every, algo=1)
     pan, it_p = _sharded(X, p, P, opts, aircomp=False, check_every=check_every, algo=1,
                          panels=True)
     assert it_r == it_p and len(it_p) == 1
-    assert torch.equal(rows, pan)
+    assert rel_l2(rows.cpu().numpy(), pan.cpu().numpy()) <= 1e-6
 
 
 def test_sharded_gm_panels_philox():

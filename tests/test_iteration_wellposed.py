@@ -31,7 +31,8 @@ from oracle import aggregators as orc
 
 MODULES = ["test_gpu_batched", "test_gpu_resident_batched", "test_gpu_weiszfeld",
            "test_gpu_panels", "test_gpu_sharded", "test_gpu_distributed", "test_gpu_fullsize",
-           "test_gpu_c5_fullsize", "test_gpu_resident_hier", "test_gpu_emnist_fullsize"]
+           "test_gpu_c5_fullsize", "test_gpu_resident_hier", "test_gpu_emnist_fullsize",
+           "test_gpu_rows_pass"]
 
 
 def _cases():
