@@ -8,7 +8,7 @@ BUILD    := build/obj
 LIB      := byzantine_aircomp_amd/libgmagg.so
 HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-result \
             -I include -munsafe-fp-atomics
-SRCS     := $(CSRC)/stream_pass.hip $(CSRC)/rows_pass.hip $(CSRC)/gram.hip $(CSRC)/resident.hip $(CSRC)/resident_batched.hip $(CSRC)/coordinate.hip $(CSRC)/weiszfeld.hip $(CSRC)/oma.hip $(CSRC)/pack.hip $(CSRC)/clients.hip $(CSRC)/api.hip
+SRCS     := $(CSRC)/stream_pass.hip $(CSRC)/gram.hip $(CSRC)/resident.hip $(CSRC)/resident_batched.hip $(CSRC)/coordinate.hip $(CSRC)/weiszfeld.hip $(CSRC)/oma.hip $(CSRC)/pack.hip $(CSRC)/clients.hip $(CSRC)/api.hip $(CSRC)/rows_pass.hip
 OBJS     := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(SRCS))
 HDRS     := $(wildcard $(CSRC)/*.h) include/gmagg.h
 

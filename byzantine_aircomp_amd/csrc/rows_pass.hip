@@ -1,5 +1,5 @@
 // The fused Weiszfeld pass on the reference's own row-major [K, ldx] stack at 512 < K <= 1024
-// (round 6): the drop-in layout's STEP / INIT for gm2 (M:174-181, stream_pass.hip's algorithm).
+// (round 6): the drop-in layout's STEP pass for gm2 (M:174-181, stream_pass.hip's algorithm).
 //
 // Why a second kernel for the same arithmetic.  On row-major X every 128-byte row segment of
 // a chunk lies in its own 2 MB page (rows are 4 * ldx bytes apart), so the per-CU address
@@ -192,8 +192,8 @@ __global__ void __launch_bounds__(kRW * 64, 8) rows_pass(PassArgs a) {
   }
 }
 
-// GMAGG_ROWS_LEAN (read per call): 1 (default) this kernel for the row-major gm2 passes it
-// covers, 0 the generic stream_pass tile (A/B, tests)
+// GMAGG_ROWS_LEAN (read per call): 1 (default) this kernel for the row-major gm2 STEP passes,
+// 2 the INIT pass too, 0 the generic stream_pass tile (A/B, tests)
 static bool rows_lean_on() {
   const char* e = getenv("GMAGG_ROWS_LEAN");
   return e ? atoi(e) != 0 : true;
@@ -201,7 +201,14 @@ static bool rows_lean_on() {
 
 bool rows_pass_eligible(const PassArgs& a, int mode) {
   // the lane offsets are 32-bit: (rows per group - 1) * ldx + d floats in bytes
-  return rows_lean_on() && a.panel_stride == 0 && a.noise == 0 && (mode == 0 || mode == 1) &&
+  // STEP only: the INIT pass stays on the generic tile so that gm2 with the fused OMA
+  // pre-noise (INIT mode 4, generic) and OMA followed by gm2 (INIT mode 1) keep computing the
+  // initial distances identically — the fused form equals the separate one bit for bit
+  // (tests/test_gpu_weiszfeld.py); the INIT template stays built for A/B (GMAGG_ROWS_LEAN=2)
+  const char* e = getenv("GMAGG_ROWS_LEAN");
+  const bool init_too = e && atoi(e) == 2;
+  return rows_lean_on() && a.panel_stride == 0 && a.noise == 0 &&
+         (mode == 0 || (mode == 1 && init_too)) &&
          a.K > 512 && a.K <= kRG * kRR && a.d % 4 == 0 && a.ldx % 4 == 0 &&
          (reinterpret_cast<uintptr_t>(a.X) & 15) == 0 &&
          ((uint64_t)a.ldx * (kRQ - 1) + (uint64_t)a.d) * 4u < (1ull << 31);

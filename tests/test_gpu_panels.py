@@ -61,13 +61,14 @@ def test_panels_bit_identical_to_rows(K, d, agg):
         # 32 < K <= 64 and 128 < K <= 256 panels have a tile of their own, api.hip pick_cfg;
         # row-major gm2 at 512 < K <= 1024 runs the 32-wave rows kernel, rows_pass.hip,
         # whose column sums take another order: equal to rounding)
+        assert (ra.iters, ra.converged) == (rb.iters, rb.converged)
         if agg == "gm2" and 512 < K <= 1024:
             assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 1e-6
+            assert abs(ra.last_movement - rb.last_movement) <= 1e-3 * rb.last_movement
         else:
             assert torch.equal(a, b)
-        assert (ra.iters, ra.converged) == (rb.iters, rb.converged)
-        assert ra.last_movement == rb.last_movement or (np.isnan(ra.last_movement)
-                                                        and np.isnan(rb.last_movement))
+            assert ra.last_movement == rb.last_movement or (np.isnan(ra.last_movement)
+                                                            and np.isnan(rb.last_movement))
     else:
         # row-major runs another tile here (float2/float1 for d % 4 != 0, or the
         # wider INIT tile): other summation grouping, equal to rounding
