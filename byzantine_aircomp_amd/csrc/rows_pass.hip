@@ -200,7 +200,6 @@ static bool rows_lean_on() {
 }
 
 bool rows_pass_eligible(const PassArgs& a, int mode) {
-  // the lane offsets are 32-bit: (rows per group - 1) * ldx + d floats in bytes
   // STEP only: the INIT pass stays on the generic tile so that gm2 with the fused OMA
   // pre-noise (INIT mode 4, generic) and OMA followed by gm2 (INIT mode 1) keep computing the
   // initial distances identically — the fused form equals the separate one bit for bit
@@ -211,7 +210,9 @@ bool rows_pass_eligible(const PassArgs& a, int mode) {
          (mode == 0 || (mode == 1 && init_too)) &&
          a.K > 512 && a.K <= kRG * kRR && a.d % 4 == 0 && a.ldx % 4 == 0 &&
          (reinterpret_cast<uintptr_t>(a.X) & 15) == 0 &&
-         ((uint64_t)a.ldx * (kRQ - 1) + (uint64_t)a.d) * 4u < (1ull << 31);
+         // a group's 8 rows (the resource's size) below 2^31 bytes, so the out-of-range lane
+         // offset 0x80000000 is past every resource and reads 0
+         (uint64_t)a.ldx * kRQ * 4u < (1ull << 31);
 }
 
 hipError_t launch_rows_pass(int mode, int grid, const PassArgs& a, hipStream_t s) {
