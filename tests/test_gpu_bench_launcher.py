@@ -56,3 +56,23 @@ def test_bench_two_ranks_c3_small():
     assert cfg["parallelism"].startswith("d-shard x2"), cfg
     assert line["check"]["ok"], line["check"]
     assert cfg["iters"] == want_iters, (cfg["iters"], want_iters)
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_ranks_c5_sweep():
+    """The C5 sweep through the launcher at N = 2: each rank takes its contiguous share of
+    every var group (bench.c5_rank_slice), no data-path collective, max-over-ranks timing."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--one-gpu",
+                        "--workload", "c5", "--problems", "32", "--steps", "1", "--warmup", "1",
+                        "--no-cpu", "--soak", "0", "--alt-steps", "0"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=500)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = json.loads(lines[0])
+    cfg = line["config"]
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert cfg["problems"] == 32 and cfg["problems_per_rank"] == 16, cfg
+    assert line["check"]["ok"], line["check"]

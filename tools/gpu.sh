@@ -34,7 +34,9 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest -m gpu -q -x --timeout 120 --timeout-method thread \
         ${rest:-tests} > "$out/pytest_gpu.log" 2>&1
       rc=$?; tail -3 "$out/pytest_gpu.log"
-      [ $rc -ne 0 ] && { grep -E "^(FAILED|ERROR)|Error|assert" "$out/pytest_gpu.log" | head -20; exit $rc; }
+      if [ $rc -ne 0 ]; then
+        grep -E "^(FAILED|ERROR)|Error|assert" "$out/pytest_gpu.log" | head -20; exit $rc
+      fi
       ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 \
