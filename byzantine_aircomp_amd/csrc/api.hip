@@ -356,6 +356,17 @@ int pick_vec(const float* X, int64_t d, int64_t ldx) {
   return 1;
 }
 
+// PassArgs.chunk_pair for a row-major pass of `grid` blocks on tile `cfg`: the CU count when
+// the grid is exactly two blocks per CU (GMAGG_CHUNK_PAIR=0: off, for A/B).  Only the 32-wave
+// rows kernel reads it (the generic tile's chunk order, and so its sums, stay as they were)
+int chunk_pair(const gm_ctx* c, const PassCfg& cfg, int64_t grid) {
+  static const bool off = [] {
+    const char* e = getenv("GMAGG_CHUNK_PAIR");
+    return e && atoi(e) == 0;
+  }();
+  return !off && cfg.OCC == 2 && grid == 2 * (int64_t)c->num_cu ? c->num_cu : 0;
+}
+
 int record_pass_begin(gm_ctx* c, hipStream_t s, hipEvent_t* e0, hipEvent_t* e1) {
   *e0 = *e1 = nullptr;
   if (!c->timing) return GM_OK;
@@ -1133,6 +1144,7 @@ int gm_weiszfeld_f32(gm_ctx* c, const float* X, int64_t K, int64_t d, int64_t ld
       a.slab = w.slab; a.slab_stride = S;
       a.noise = noise_kind; a.hnoise = w.hnoise; a.seed = o->seed; a.iter = t; a.col_off = col_off;
       a.panel_stride = panels ? ldx : 0;
+      a.chunk_pair = panels ? 0 : chunk_pair(c, init ? cfg_i : cfg, init ? nb_init : nb_step);
       int mode = init ? init_mode : 0;
       if (init && oma_pending) {
         // the fused OMA needs float4 groups = Philox blocks: V = 4, 4-aligned shards

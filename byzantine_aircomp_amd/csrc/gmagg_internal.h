@@ -60,7 +60,22 @@ struct PassArgs {
   // oma_seed (+ p * kSeedStride for batched problem p), draws as gm_oma_philox_f32's
   float oma_sd;
   uint64_t oma_seed;
+  // rows_pass only (the row-major gm2 STEP at two blocks per CU): P = the CU count when the
+  // grid is two blocks per CU, else 0.  The hardware places block b and block b + P on one
+  // CU, so they take adjacent chunks (first_chunk): the CU's two blocks read the same rows'
+  // 2 MB pages at about the same time (round 6: C3 rows STEP 6,844 -> 6,788 us; pairing b
+  // with b + 8 or b + 16 gains nothing, and on panels the pairing measured 1.6 % slower:
+  // profiles/r6s2_rows_chunk_pair_ab.jsonl)
+  int chunk_pair;
 };
+
+// The first chunk of block b in a grid-stride walk (chunks b', b' + grid, ...): b itself,
+// or with the pairing above 2 (b mod P) + (b / P) for b < 2P (a permutation of [0, grid)
+// when 2P divides the grid)
+__host__ __device__ inline int64_t first_chunk(int P, int64_t b, int64_t grid) {
+  if (P <= 0 || grid % (2 * P) != 0) return b;
+  return 2 * ((b / (2 * P)) * P + b % P) + (b / P) % 2;
+}
 
 constexpr uint64_t kSeedStride = 0x9E3779B97F4A7C15ull;
 // The reference's fp32 movement floor in ulps of ||g|| (M:180: an fp32 norm of a difference

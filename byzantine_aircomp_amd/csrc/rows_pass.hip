@@ -88,6 +88,7 @@ __global__ void __launch_bounds__(kRW * 64, 8) rows_pass(PassArgs a) {
   };
   int par = 0;
   int64_t ch = blockIdx.x;
+  ch = first_chunk(a.chunk_pair, blockIdx.x, grid);
   {
     const uint32_t off = lane_off(ch);
 #pragma unroll
