@@ -62,10 +62,11 @@ struct PassArgs {
   uint64_t oma_seed;
   // rows_pass only (the row-major gm2 STEP at two blocks per CU): P = the CU count when the
   // grid is two blocks per CU, else 0.  The hardware places block b and block b + P on one
-  // CU, so they take adjacent chunks (first_chunk): the CU's two blocks read the same rows'
-  // 2 MB pages at about the same time (round 6: C3 rows STEP 6,844 -> 6,788 us; pairing b
-  // with b + 8 or b + 16 gains nothing, and on panels the pairing measured 1.6 % slower:
-  // profiles/r6s2_rows_chunk_pair_ab.jsonl)
+  // CU, so they take adjacent chunks (first_chunk): the CU's two blocks read adjacent 128-B
+  // segments of each row at about the same time (round 6: C3 rows STEP 6,844 -> 6,788 us,
+  // with identical UTCL1 misses: DRAM / L2 locality; pairing b with b + 8 or b + 16 gains
+  // nothing, and on panels the pairing measured 1.6 % slower:
+  // profiles/r6s2_rows_chunk_pair_ab.jsonl, r6s2_utcl1_rows_chunk_pair.json)
   int chunk_pair;
 };
 
