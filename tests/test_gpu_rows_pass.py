@@ -83,3 +83,23 @@ def iteration_cases():
         Xs, g0 = _recipe(K, d, K + d, ldx)
         return [(Xs[:, :d].contiguous(), g0, 1000, 1e-5)]
     return [(f"rows_pass_{K}x{d}", lambda K=K, d=d, ldx=ldx: case(K, d, ldx)) for K, d, ldx in CASES]
+
+
+@pytest.mark.parametrize("val", [float("nan"), float("inf"), -float("inf")])
+@pytest.mark.parametrize("layout", ["rows", "panels"])
+def test_rows_pass_special_values(val, layout):
+    """One NaN / +-inf element (NaN is never <= tol, so the call runs to
+    maxiter): the reference's iterate turns all-NaN — an infinite row gets weight 0 and
+    0 * inf = NaN in its column, then every distance is NaN — and so does the 32-wave rows
+    kernel's (and the panel tile's), after the same maxiter iterations."""
+    import byzantine_aircomp_amd as bz
+    X, g0 = _recipe(600, 4096, 11)
+    X[17, 123] = val
+    opts = {"maxiter": 7, "tol": 1e-5, "guess": g0.clone()}
+    want, tr = orc.gm2(X.clone(), dict(opts))
+    Xd = X.cuda() if layout == "rows" else bz.ClientPanels.from_rows(X.cuda())
+    out = bz.gm2(Xd, dict(opts, guess=g0.cuda()))
+    r = bz.aggregators.last_result
+    assert r.algo == "stream" and r.iters == tr.iters == 7, (r, tr)
+    assert torch.equal(torch.isnan(out.cpu()), torch.isnan(want))
+    assert torch.isnan(out).all()
