@@ -87,8 +87,7 @@ __global__ void __launch_bounds__(kRW * 64, 8) rows_pass(PassArgs a) {
     gold = (tid < kRJ && ch < nch && gj < d) ? a.g_old[gj] : 0.f;
   };
   int par = 0;
-  int64_t ch = blockIdx.x;
-  ch = first_chunk(a.chunk_pair, blockIdx.x, grid);
+  int64_t ch = first_chunk(a.chunk_pair, blockIdx.x, grid);   // chunks ch, ch + grid, ...
   {
     const uint32_t off = lane_off(ch);
 #pragma unroll
