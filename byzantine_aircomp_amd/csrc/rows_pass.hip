@@ -20,6 +20,9 @@
 //
 // Thread map: wave w, lane = 8 q + c: column group c (4 columns, 16 B), row group
 // rg = 8 w + q; rows rg + 128 i, i < 8.  A wave instruction reads 8 rows x 128 B.
+// Chunk order: grid-stride, except that the two blocks one CU holds (b, b + #CUs) take
+// adjacent chunks when the grid is two blocks per CU (PassArgs.chunk_pair; STEP 6,844 ->
+// 6,788 us at C3, profiles/r6s2_rows_chunk_pair_ab.jsonl).
 #include "device_util.h"
 #include "gmagg_internal.h"
 
