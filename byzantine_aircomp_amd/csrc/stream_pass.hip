@@ -389,17 +389,20 @@ static const void* pass_fn(bool panel) {
   // Measured on MI355X (profiles/history/r01_ab_pass.txt, r01_pipe_sweep.txt): the plain
   // pass is as fast or faster than the two-tile PIPE variant at every K, so that
   // one is only built with -DGMK_PIPE_VARIANT for A/B runs.
-  // Panels: the rolling-prefetch STEP pass (6.44-6.56 vs 6.63 ms at C3).  INIT stays
-  // plain: with the guess on the finisher threads (one load per column instead of
-  // one per lane) plain INIT runs at STEP's time, 6.33 vs 6.33 ms, and the rolling
-  // INIT gains nothing, 6.29-6.65 vs STEP 6.32-6.56 (profiles/history/r2_init_ab.txt).
+  // Panels: the rolling-prefetch STEP pass (6.44-6.56 vs 6.63 ms at C3), and since round 6
+  // the INIT pass too (mode 1 / 2; the fused-OMA INIT, mode 4, stays plain): the plain INIT
+  // ran 117-128 us above the STEP pass at C3 in three of four interleaved pairs (12 in the
+  // first), the rolling one 32-48 us (profiles/r6s3_init_roll_ab.jsonl; round 2 had measured no
+  // gain, profiles/history/r2_init_ab.txt).  The schedule moves loads, not arithmetic: the
+  // results are the same bits.
   constexpr bool kRollDefault = MODE == 0;
+  constexpr bool kRollPanel = kRollDefault || MODE == 1 || MODE == 2;
   if constexpr (V == 4) {
     if (panel) {
       const int pv = pass_variant();
       if (pv == 3)
         return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 3, OCC, true>);
-      if (pv == 2 || (pv < 0 && kRollDefault))
+      if (pv == 2 || (pv < 0 && kRollPanel))
         return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 2, OCC, true>);
       return reinterpret_cast<const void*>(&weiszfeld_pass<V, NW, LPR, R, MODE, 0, OCC, true>);
     }
