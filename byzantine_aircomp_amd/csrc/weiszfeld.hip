@@ -27,9 +27,23 @@ __global__ void __launch_bounds__(1024) slab_reduce(const double* __restrict__ s
   __shared__ double red[32][33];
   const int cx = threadIdx.x & 31, by = threadIdx.x >> 5;
   const int64_t j = (int64_t)blockIdx.x * 32 + cx;
+  // rows by, by + 32, ... summed in that order; their loads issued 16 at a time (a
+  // dependent load per add made this latency-bound: round 6, 6.9 us at nb = 512)
   double acc = 0.0;
-  if (j < S)
-    for (int b = by; b < nb; b += 32) acc += slab[(int64_t)b * S + j];
+  if (j < S) {
+    constexpr int U = 16;
+    for (int b0 = by; b0 < nb; b0 += 32 * U) {
+      double v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int b = b0 + 32 * u;
+        v[u] = b < nb ? slab[(int64_t)b * S + j] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (b0 + 32 * u < nb) acc += v[u];
+    }
+  }
   red[by][cx] = acc;
   __syncthreads();
   if (by == 0 && j < S) {
